@@ -1,0 +1,150 @@
+"""Pin the CPU oracle (oracle/vad_oracle.py) against the golden vectors that
+tests/golden/gen_golden.py produced by running the unmodified reference."""
+import numpy as np
+import pytest
+
+from oracle import vad_oracle as O
+
+
+def frame_rel(a, b):
+    """Per-frame L2-relative error (SURVEY.md 8(c) tolerance definition)."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-300)
+
+
+@pytest.mark.parametrize("name", ["fb_26", "fb_40", "fb_20_0_8000", "fb_32_100_4000"])
+def test_filterbanks(golden, name):
+    g = golden("filterbanks")
+    lo, hi, nf, sr = g[name + "_params"]
+    fb = O.get_mel_filterbanks(lo, hi, 512, int(nf), sr)
+    np.testing.assert_array_equal(fb, g[name])
+    hz = O.hz_from_mel(O.mel_from_hz(lo, hi, int(nf)))
+    np.testing.assert_array_equal(O.convert_to_fft_bins(sr, hz, 512), g[name + "_bins"])
+
+
+def test_fb26_structure(golden):
+    fb = golden("filterbanks")["fb_26"]
+    assert (fb != 0).sum() == 444
+    assert ((fb != 0).sum(axis=0) <= 2).all()  # each bin feeds at most two filters
+
+
+def test_spec_mag_exact(golden):
+    g = golden("frames")
+    spec = O.spec_batch(g["frames"])
+    np.testing.assert_array_equal(spec, g["spec"])  # same pocketfft float32 path
+    for i, f in enumerate(g["frames"][:8]):
+        np.testing.assert_array_equal(O.get_spec_mag(f), g["spec"][i])
+
+
+@pytest.mark.parametrize("nf,key", [(26, "mfcc26"), (40, "mfcc40")])
+def test_mfcc_from_spec(golden, nf, key):
+    g = golden("frames")
+    fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+    m = O.get_mfcc_from_spec(g["spec"], fb, 13)
+    ref = g[key]
+    # fp64 restatement of scipy's DCT: per-frame agreement far inside 1e-4
+    assert frame_rel(m, ref).max() < 1e-12
+    # digital silence: c0 = log10(eps)*sqrt(n_filters)
+    assert abs(ref[0, 0] - np.log10(np.finfo(float).eps) * np.sqrt(nf)) < 1e-9
+
+
+@pytest.mark.parametrize("L", [800, 512, 256, 401])
+def test_other_frame_lengths(golden, L):
+    g = golden("frames")
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    fr = g[f"frames_{L}"]
+    np.testing.assert_array_equal(O.spec_batch(fr), g[f"spec_{L}"])
+    m = np.stack([O.get_mfcc(f, 512, fb, 13) for f in fr])
+    assert frame_rel(m, g[f"mfcc26_{L}"]).max() < 1e-12
+
+
+def test_framing_counts(golden):
+    g = golden("clip")
+    for L, c in zip(g["lens"], g["counts"]):
+        assert O.n_frames(int(L)) == c
+        assert len(O.split_into_frames(np.zeros(int(L)))) == c
+        assert len(O.frame_matrix(np.zeros(int(L), np.float32))) == c
+
+
+def test_offline_features(golden):
+    g = golden("clip")
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    m = O.mfcc_batch(g["clip"], fb)
+    assert frame_rel(m, g["mfcc"]).max() < 1e-12
+    f = O.offline_features(m)
+    ref = g["features"]
+    assert f.shape == ref.shape == (93, 3, 13)
+    assert frame_rel(f.reshape(len(f), -1), ref.reshape(len(ref), -1)).max() < 1e-12
+
+
+def _layers(w, prefix, n, b_last=None):
+    lay = [(w[f"{prefix}_W{i}"], w[f"{prefix}_b{i}"]) for i in range(n)]
+    if b_last is not None:
+        lay[-1] = (lay[-1][0], b_last)
+    return lay
+
+
+def test_analyser_trace(golden):
+    g = golden("analyser")
+    w = golden("ffn")
+    lay = _layers(w, "ref39", 4)
+    an = O.AnalyserOracle(O.FFNPredictor(lay))
+    an.load_init_inactive_frames(list(g["noise"]))
+    stream = list(g["stream"])
+    rets, feats = [], []
+    for f in stream:
+        if len(an.frames_buffer) == 5:
+            feats.append(an.features())
+        r = an.feed_frame(f)
+        rets.append(-1 if r is None else next(i for i, s in enumerate(stream) if s is r))
+    np.testing.assert_array_equal(rets, g["returns"])
+    fx = np.asarray(feats)
+    ref = g["features"]
+    # Constant (digital-silence) windows: std = 0 -> 0/0 = NaN.  Which of the
+    # 13 coefficients come out NaN depends on the last-ulp noise of each DCT
+    # implementation (c1..c12 of a constant log-energy vector are ~1e-14), but
+    # every such row holds a NaN, so its label is 0 either way.
+    nan_rows = np.isnan(ref).any(axis=1)
+    np.testing.assert_array_equal(np.isnan(fx).any(axis=1), nan_rows)
+    assert nan_rows.sum() >= 5
+    assert np.allclose(fx[~nan_rows], ref[~nan_rows], rtol=1e-9, atol=1e-9)
+
+
+def test_analyser_errors(golden):
+    g = golden("analyser")
+    w = golden("ffn")
+    assert str(g["error_noinit"]) == "0:TypeError"
+    assert str(g["error_badinit"]) == "ValueError"
+    an = O.AnalyserOracle(O.FFNPredictor(_layers(w, "ref39", 4)))
+    with pytest.raises(TypeError):
+        an.feed_frame(g["stream"][0])
+    with pytest.raises(ValueError):
+        an.load_init_inactive_frames(list(g["noise"][:4]))
+    an = O.AnalyserOracle(O.FFNPredictor(_layers(w, "ref39", 4, w["ref39_b3_music"])))
+    an.load_init_inactive_frames(list(g["noise"]))
+    k = int(str(g["error_music"]).split(":")[0])
+    for f in g["stream"][:k]:
+        an.feed_frame(f)
+    with pytest.raises(AssertionError):
+        an.feed_frame(g["stream"][k])
+
+
+def test_ffn_labels(golden):
+    w = golden("ffn")
+    x = w["test_x"]
+    np.testing.assert_array_equal(O.ffn_labels(x, _layers(w, "ref39", 4)), w["test_labels_ref39"])
+    np.testing.assert_array_equal(O.ffn_labels(x[:, :13], _layers(w, "bl13", 3)),
+                                  w["test_labels_bl13"])
+    # the fixture features are the analyser features of the fixture clip
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    fx = O.analyser_features(O.mfcc_batch(w["test_clip"], fb))
+    np.testing.assert_array_equal(np.isnan(fx).any(axis=1), np.isnan(x).any(axis=1))
+
+
+def test_nan_label_is_zero():
+    lay = [(np.ones((39, 4), np.float32), np.zeros(4, np.float32)),
+           (np.ones((4, 3), np.float32), np.array([0, 5, 1], np.float32))]
+    x = np.ones((2, 39))
+    x[0, 5] = np.nan
+    assert list(O.ffn_labels(x, lay)) == [0, 1]
