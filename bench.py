@@ -1,0 +1,192 @@
+"""Benchmark: MFCC+FFN frames/s on synthetic 16 kHz audio (BASELINE.json).
+
+Workload (one step, per rank): one clip of F = 1,000,000 frames of 25 ms at a
+10 ms hop (160*(F-1)+401 fp32 samples, already resident in HBM), framed ->
+MFCC (HIP kernel) -> 5-frame analyser features + FFN on f32 MFMA (HIP
+kernel) -> F-5 uint8 labels; with N > 1 ranks each rank classifies its own
+clip (weak scaling, no data-path collective) and the per-window decisions are
+gathered to rank 0 over RCCL inside the step (BASELINE configs 3 and 4).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--ffn bl13|ref39]
+
+Rank 0 prints ONE JSON line.  `value` = frames (MFCC frames) processed by all
+ranks / max-over-ranks wall time of the K timed steps.  `roofline` is for the
+dominant kernel (the MFCC kernel), timed with HIP events on the stream it is
+launched on; `cpu_baseline` times the oracle's vectorised NumPy restatement
+on a bounded sample on one host core (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFCC_BYTES_PER_FRAME = 160 * 4 + 13 * 4   # new samples in + 13 fp32 out
+FFN_BYTES_PER_FRAME = 13 * 4 + 1          # MFCC row in + uint8 label out
+
+
+def synth_audio(n_samples, seed, device):
+    """int16-range noise with per-1600-sample amplitude 10**U(0,4), 5% silent
+    segments; generated on the device."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    seg = 1600
+    n_seg = (n_samples + seg - 1) // seg
+    amp = 10.0 ** (torch.rand(n_seg, generator=g, device=device) * 4.0)
+    amp[torch.rand(n_seg, generator=g, device=device) < 0.05] = 0.0
+    x = torch.randn(n_seg * seg, generator=g, device=device) * amp.repeat_interleave(seg)
+    return x[:n_samples].round_().clamp_(-32767, 32767).contiguous()
+
+
+def cpu_baseline(layers, frames_per_chunk=20000, min_seconds=10.0, max_chunks=40):
+    """Oracle (NumPy restatement, test infrastructure) on one core, bounded sample."""
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits = None
+    from oracle import vad_oracle as O
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    clip = O.synth_clip(160 * (frames_per_chunk - 1) + 401, seed=1)
+    ctx = threadpool_limits(limits=1) if threadpool_limits else None
+    if ctx:
+        ctx.__enter__()
+    try:
+        n, t0 = 0, time.perf_counter()
+        while True:
+            m = O.mfcc_batch(clip, fb)
+            x = O.analyser_features_fast(m)
+            O.ffn_labels(x[:, :layers[0][0].shape[0]], layers)
+            n += len(m)
+            el = time.perf_counter() - t0
+            if el >= min_seconds or n >= frames_per_chunk * max_chunks:
+                break
+    finally:
+        if ctx:
+            ctx.__exit__(None, None, None)
+    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames ({n // frames_per_chunk} x {frames_per_chunk}-frame synthetic "
+                      f"clips), oracle/vad_oracle.py vectorised NumPy (pocketfft f32 FFT, fp64 "
+                      f"mel/log/DCT, fp64 features + FFN), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=1_000_000)
+    ap.add_argument("--ffn", default="bl13", choices=["bl13", "ref39"])
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.dist import gather_labels
+
+    topo = TOPOLOGY_BL13 if args.ffn == "bl13" else TOPOLOGY_REF39
+    layers = random_layers(topo, seed=3)
+    pipe = VadPipeline(FFNClassifier(layers))
+    F = args.frames
+    n_samples = 160 * (F - 1) + 401
+    audio = synth_audio(n_samples, 100 + rank, dev)
+    assert pipe.n_frames(audio.numel()) == F
+    mfcc = torch.empty((F, 13), dtype=torch.float32, device=dev)
+    labels = torch.empty((F - 5,), dtype=torch.uint8, device=dev)
+    ffn_plan = pipe.ffn.plan
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        pipe.mfcc(audio, out=mfcc)                       # HIP MFCC kernel
+        if ev is not None:
+            ev[1].record(stream)
+        ffn_plan.window_labels(mfcc, out=labels)          # HIP features + MFMA FFN kernel
+        if ev is not None:
+            ev[2].record(stream)
+        if world > 1:
+            gather_labels(labels)                          # RCCL: decisions -> rank 0
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    mfcc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    ffn_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+
+    if rank == 0:
+        value = world * F * args.steps / el
+        dom_ms, dom_bytes, dom = (mfcc_ms, MFCC_BYTES_PER_FRAME, "mfcc_kernel") \
+            if mfcc_ms >= ffn_ms else (ffn_ms, FFN_BYTES_PER_FRAME, "ffn_kernel")
+        achieved = dom_bytes * F / (dom_ms * 1e-3) / 1e9
+        traffic = None
+        tp = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tp):
+            with open(tp) as f:
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        out = {
+            "metric": "MFCC+FFN frames/sec on 16 kHz 25 ms/10 ms hop",
+            "value": value,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (int16-range noise, 10**U(0,4) segment gains, 5% digital silence; "
+                    "seeded random-init FFN weights)",
+            "config": {"workload": "C3/C4: MFCC + FFN VAD forward, 1 clip of F frames per GPU "
+                                   "(25 ms frames, 10 ms hop, 512-pt FFT, 26 mel, 13 MFCC, "
+                                   "analyser 5-frame features), labels gathered to rank 0",
+                       "frames_per_gpu": F, "ffn": "-".join(map(str, topo)),
+                       "parallelism": f"clip-shard x{world}"},
+            "roofline": {"bound": "hbm", "kernel": dom,
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": dom_bytes * F,
+                         "avg_launch_ms": dom_ms},
+            "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms},
+        }
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = cpu_baseline(layers)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,147 @@
+/*
+ * vad_amd.h -- C ABI of libvad_amd.so, the MI355X-native MFCC + FFN VAD path.
+ *
+ * The reference (nameofuser1/vad) is pure Python with no FFI, so there is no
+ * existing binding to match byte for byte; each entry point below names the
+ * reference function whose semantics it implements (file:line in the
+ * reference tree) and the Python host layer (vad_amd/, ctypes) that mirrors
+ * the reference API on top of it.
+ *
+ * Conventions
+ *   - All data pointers are DEVICE pointers owned by the caller (torch tensors
+ *     on the host side).  Plans own small device buffers of their own.
+ *   - `stream` is a hipStream_t passed as void* (0 = the null stream).
+ *   - No allocation, no host synchronisation on any hot call: every hot call
+ *     is capturable into a hipGraph.
+ *   - Return value: 0 on success, a negative VAD_E* code for argument
+ *     errors, or a positive hipError_t from the HIP runtime.
+ */
+#ifndef VAD_AMD_H
+#define VAD_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VAD_MAX_FILTERS 64
+#define VAD_MAX_MFCC 16
+#define VAD_MAX_TAPS 4096
+#define VAD_FFT_N 512
+#define VAD_MAX_FFN_LAYERS 4
+
+#define VAD_OK 0
+#define VAD_EINVAL (-1)        /* bad argument (null, negative size, ...) */
+#define VAD_EUNSUPPORTED (-2)  /* valid for the reference, not built here (fft_n != 512, ...) */
+#define VAD_ENOMEM (-3)
+
+typedef struct vad_mfcc_plan vad_mfcc_plan;
+typedef struct vad_ffn_plan vad_ffn_plan;
+
+/* Library version string. */
+const char* vad_version(void);
+
+/* Number of frames split_into_frames() yields: frames are taken while
+ * len - offset > frame_size (reference dataset/file_processing.py:99). */
+int64_t vad_n_frames(int64_t n_samples, int32_t frame_size, int32_t hop);
+
+/* ---------------------------------------------------------------------------
+ * MFCC plan.  Replaces the per-call arguments of mfcc.get_mfcc /
+ * get_mfcc_from_spec (reference mfcc.py:67-78): the (n_filters, 256)
+ * filterbank from get_mel_filterbanks (mfcc.py:39-56, built on the host in
+ * fp64 exactly as the reference does), the MFCC count (mfcc.py:76 [:mfcc_n])
+ * and the lifter length (mfcc.py:85, L=22 in every reference call).
+ * fft_n must be 512 (mfcc.py:61 with the reference's only value, config.py:27).
+ * ------------------------------------------------------------------------- */
+int vad_mfcc_plan_create(const double* filterbank_host, int32_t n_filters, int32_t fft_n,
+                         int32_t mfcc_n, int32_t lifter_L, vad_mfcc_plan** out);
+int vad_mfcc_plan_destroy(vad_mfcc_plan* plan);
+
+/* Frames f = 0..n_frames-1 start at src + f*frame_stride and hold frame_len
+ * samples (fp32); only the first min(frame_len, 512) feed the 512-point FFT
+ * (np.fft.fft(x, 512) zero-pads / truncates, mfcc.py:61).
+ * A clip framed at hop H is frame_stride = H, frame_len = 400
+ * (file_processing.py:80-103); a frame matrix is frame_stride = row length. */
+
+/* get_spec_mag (mfcc.py:59-61) of every frame -> spec[f*256 + k], fp32. */
+int vad_spec_f32(const vad_mfcc_plan* plan, const float* src, int64_t frame_stride,
+                 int32_t frame_len, int64_t n_frames, float* spec, void* stream);
+
+/* get_mfcc (mfcc.py:67-69) of every frame -> mfcc[f*mfcc_n + c], fp32. */
+int vad_mfcc_f32(const vad_mfcc_plan* plan, const float* src, int64_t frame_stride,
+                 int32_t frame_len, int64_t n_frames, float* mfcc, void* stream);
+
+/* get_mfcc_from_spec (mfcc.py:72-78) of n spectra spec[f*256 + k]. */
+int vad_mfcc_from_spec_f32(const vad_mfcc_plan* plan, const float* spec, int64_t n,
+                           float* mfcc, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * FFN plan: a Keras Sequential of Dense layers with ReLU between them and a
+ * softmax at the end, predicted class = argmax (reference
+ * learning/ffn_trainer.py:106-116; config.py:45-47 labels).  Weights are
+ * Keras-layout W (in, out) row-major fp32 and b (out).  Constraints of this
+ * build: 1..4 layers, in_dim <= 64, hidden <= 64, classes <= 4.
+ * ------------------------------------------------------------------------- */
+int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims /* n_layers+1 */,
+                        const float* const* W_host, const float* const* b_host,
+                        vad_ffn_plan** out);
+int vad_ffn_plan_destroy(vad_ffn_plan* plan);
+
+/* Feature rows (reference feature layout, 39 = 3 x 13):
+ *   mode VAD_FEAT_ANALYSER: [Mn, M+1 - M-1, (M+2 - Mn) - (Mn - M-2)] with the
+ *     centre MFCC normalised by the 5-frame mean / std (ddof 0)
+ *     (realtime_analysis/sklearn_analyser.py:52-69,103-107);
+ *   mode VAD_FEAT_OFFLINE: [Mc, M+1 - M-1, (M+2 - Mc) - (Mc - M-2)], no
+ *     normalisation (dataset/file_processing.py:40-70).
+ * Row i is centred on MFCC frame i+2, i = 0..n_frames-6 (F-5 rows; the last
+ * full window is never emitted, exactly as both reference loops do). */
+#define VAD_FEAT_ANALYSER 0
+#define VAD_FEAT_OFFLINE 1
+
+/* features[i*3*mfcc_n + j] (fp32), i < n_frames-5. */
+int vad_features_f32(const float* mfcc, int64_t n_frames, int32_t mfcc_n, int32_t mode,
+                     float* features, void* stream);
+
+/* Labels of every analyser window: classifier.predict of the features above
+ * (sklearn_analyser.py:71) -> labels[i] (uint8), i < n_frames-5. */
+int vad_features_ffn(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frames,
+                     int32_t mfcc_n, int32_t mode, uint8_t* labels, void* stream);
+
+/* FFN forward over caller-built feature rows x[i*in_dim + j] (predict on a
+ * batch, ffn_trainer.py:106-116) -> labels[i]. */
+int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t* labels,
+                    void* stream);
+
+/* Clip path: framing + MFCC + features + FFN (dataset_creator/process_file
+ * framing, file_processing.py:38-70, with the analyser's classifier call,
+ * sklearn_analyser.py:71).  labels[i] for windows i < n_frames-5 of the clip.
+ * `workspace` (device, >= vad_mfcc_ffn_workspace_bytes()) holds intermediate
+ * MFCCs when the build does not keep them on chip; 0 bytes when fused. */
+size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, int64_t n_samples,
+                                    int32_t frame_size, int32_t hop);
+int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
+                 int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
+                 uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Streaming: S independent analyser streams advanced by one frame each
+ * (SKLearnAnalyzer.feed_frame, sklearn_analyser.py:46-82, for S streams at
+ * once).  State lives in device buffers the caller allocates with the sizes
+ * below; every stream's state is independent.
+ *   frames[s*frame_stride + t], t < frame_len: the new frame of stream s.
+ *   ring: (S, 5, mfcc_n) fp32 MFCC ring; count: (S,) int32 frames seen.
+ * After the call, labels[s] = class of the window centred 3 calls ago, or
+ * 255 while the stream has seen fewer than 5 frames before this one
+ * (feed_frame returns None for its first 5 calls, :48-50).
+ * ------------------------------------------------------------------------- */
+int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n);
+int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
+                    int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
+                    int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VAD_AMD_H */

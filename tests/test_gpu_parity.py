@@ -1,0 +1,376 @@
+"""HIP path vs the oracle / reference golden vectors (needs an MI355X).
+
+Tolerances:
+  MFCC   per frame  ||d||_2 / ||ref||_2 <= 1e-4  and  max|d| <= 1e-4 * max|ref|
+  spec   per frame  ||d||_2 / ||ref||_2 <= 1e-5 (float32 FFTs, different orders)
+  labels bit-exact wherever the fp64 oracle's top-2 logit margin exceeds
+         MARGIN_TOL; below it the count of disagreements is reported and bounded.
+"""
+import pickle
+
+import numpy as np
+import pytest
+
+from oracle import vad_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+MFCC_TOL = 1e-4
+SPEC_TOL = 1e-5
+MARGIN_TOL = 0.05
+
+
+def frame_rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return np.linalg.norm(a - b, axis=-1) / np.maximum(np.linalg.norm(b, axis=-1), 1e-300)
+
+
+def assert_mfcc_close(got, ref):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    assert got.shape == ref.shape
+    rel = frame_rel(got, ref)
+    mx = np.abs(got - ref).max(axis=-1) / np.abs(ref).max(axis=-1)
+    assert rel.max() <= MFCC_TOL, (rel.max(), int(rel.argmax()))
+    assert mx.max() <= MFCC_TOL, (mx.max(), int(mx.argmax()))
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def fb26():
+    return O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+
+
+def layers_from(w, prefix, n, b_last=None):
+    lay = [(w[f"{prefix}_W{i}"], w[f"{prefix}_b{i}"]) for i in range(n)]
+    if b_last is not None:
+        lay[-1] = (lay[-1][0], b_last)
+    return lay
+
+
+# ---------------------------------------------------------------------------
+# spectrum + MFCC
+# ---------------------------------------------------------------------------
+def test_spec_vs_reference(torch_cuda, golden, fb26):
+    from vad_amd.plan import MfccPlan
+    g = golden("frames")
+    t = torch_cuda.from_numpy(g["frames"]).cuda()
+    spec = MfccPlan(fb26).spec(t).cpu().numpy()
+    ref = g["spec"]
+    assert spec.dtype == np.float32 and spec.shape == ref.shape
+    silent = np.linalg.norm(ref, axis=1) == 0
+    assert np.all(spec[silent] == 0.0)
+    assert frame_rel(spec[~silent], ref[~silent]).max() <= SPEC_TOL
+
+
+@pytest.mark.parametrize("nf,key", [(26, "mfcc26"), (40, "mfcc40")])
+def test_mfcc_vs_reference(torch_cuda, golden, nf, key):
+    from vad_amd.plan import MfccPlan
+    g = golden("frames")
+    fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+    t = torch_cuda.from_numpy(g["frames"]).cuda()
+    m = MfccPlan(fb).mfcc(t).cpu().numpy()
+    assert_mfcc_close(m, g[key])
+    # digital silence: c0 = log10(eps) * sqrt(n_filters) exactly as the reference
+    assert abs(m[0, 0] - g[key][0, 0]) <= 1e-4 * abs(g[key][0, 0])
+
+
+def test_mfcc_from_spec_vs_reference(torch_cuda, golden, fb26):
+    from vad_amd.plan import MfccPlan
+    g = golden("frames")
+    s = torch_cuda.from_numpy(g["spec"]).cuda()
+    assert_mfcc_close(MfccPlan(fb26).from_spec(s).cpu().numpy(), g["mfcc26"])
+
+
+@pytest.mark.parametrize("L", [800, 512, 256, 401])
+def test_other_frame_lengths(torch_cuda, golden, fb26, L):
+    """np.fft.fft(x, 512) truncates frames > 512 and zero-pads short ones."""
+    from vad_amd.plan import MfccPlan
+    g = golden("frames")
+    fr = g[f"frames_{L}"]
+    p = MfccPlan(fb26)
+    t = torch_cuda.from_numpy(fr).cuda()
+    assert frame_rel(p.spec(t).cpu().numpy(), g[f"spec_{L}"]).max() <= SPEC_TOL
+    assert_mfcc_close(p.mfcc(t).cpu().numpy(), g[f"mfcc26_{L}"])
+    # odd stride / unaligned source exercises the scalar-load path
+    big = np.zeros((len(fr), L + 1), np.float32)
+    big[:, :L] = fr
+    tb = torch_cuda.from_numpy(big.reshape(-1)).cuda()
+    m2 = p.mfcc(tb, frame_len=L, frame_stride=L + 1, n=len(fr)).cpu().numpy()
+    assert_mfcc_close(m2, g[f"mfcc26_{L}"])
+
+
+def test_module_api_matches_reference(torch_cuda, golden, fb26):
+    """vad_amd.mfcc mirrors mfcc.py: same signatures, numpy in / out."""
+    from vad_amd import mfcc
+    g = golden("frames")
+    f = g["frames"][30]
+    s = mfcc.get_spec_mag(f, 512)
+    assert s.dtype == np.float32 and s.shape == (256,)
+    assert frame_rel(s, g["spec"][30]) <= SPEC_TOL
+    m = mfcc.get_mfcc(f, 512, fb26, 13)
+    assert m.dtype == np.float64 and m.shape == (13,)
+    assert_mfcc_close(m[None], g["mfcc26"][30][None])
+    m2 = mfcc.get_mfcc_from_spec(g["spec"][30], fb26, 13)
+    assert_mfcc_close(m2[None], g["mfcc26"][30][None])
+
+
+def test_clip_mfcc_and_offline_features(torch_cuda, golden):
+    """process_file on the fixture clip (file_processing.py:14-77)."""
+    from vad_amd.pipeline import VadPipeline
+    g = golden("clip")
+    pipe = VadPipeline()
+    clip = torch_cuda.from_numpy(g["clip"].astype(np.float32)).cuda()
+    m = pipe.mfcc(clip).cpu().numpy()
+    assert_mfcc_close(m, g["mfcc"])
+    f = pipe.process_clip(g["clip"])
+    ref = g["features"]
+    assert f.shape == ref.shape == (93, 3, 13)
+    # deltas of MFCCs: compare per row against the row's own scale
+    rel = frame_rel(f.reshape(93, -1), ref.reshape(93, -1))
+    assert rel.max() <= 10 * MFCC_TOL
+
+
+def test_framing_edge_lengths(torch_cuda, fb26):
+    from vad_amd.pipeline import VadPipeline
+    pipe = VadPipeline()
+    for L in (0, 1, 400, 401, 560, 561, 1200):
+        a = torch_cuda.from_numpy(O.synth_clip(max(L, 1), 3)[:L].copy()).cuda()
+        if L == 0:
+            a = torch_cuda.zeros(0, device="cuda")
+        m = pipe.mfcc(a).cpu().numpy()
+        assert m.shape == (O.n_frames(L), 13)
+        if len(m):
+            assert_mfcc_close(m, O.mfcc_batch(a.cpu().numpy(), fb26))
+
+
+# ---------------------------------------------------------------------------
+# features + FFN labels
+# ---------------------------------------------------------------------------
+def test_ffn_predict_bit_exact(torch_cuda, golden):
+    """fp32 MFMA forward vs the fp64 oracle on the fixture feature rows."""
+    from vad_amd.ffn import FFNClassifier
+    w = golden("ffn")
+    x = w["test_x"]
+    for prefix, n, key, dim in (("ref39", 4, "test_labels_ref39", 39),
+                                ("bl13", 3, "test_labels_bl13", 13)):
+        clf = FFNClassifier(layers_from(w, prefix, n))
+        got = clf.predict(x[:, :dim])
+        np.testing.assert_array_equal(got, w[key])
+    # NaN rows (constant windows) -> class 0
+    assert np.isnan(x).any(axis=1).sum() > 0
+
+
+def test_ffn_generic_topology(torch_cuda):
+    """A shape outside the specialised ones runs on the padded generic kernel."""
+    from vad_amd.ffn import FFNClassifier, random_layers
+    rng = np.random.default_rng(4)
+    for dims in ((20, 48, 3), (39, 10), (7, 33, 17, 5, 4)):
+        lay = random_layers(dims, seed=len(dims))
+        x = rng.standard_normal((333, dims[0])) * 2
+        ref = O.ffn_labels(x.astype(np.float32), lay)
+        marg = O.ffn_margin(x.astype(np.float32), lay)
+        got = FFNClassifier(lay).predict(x)
+        ok = marg > 1e-4
+        np.testing.assert_array_equal(got[ok], ref[ok])
+
+
+def test_analyser_features_and_labels_on_clip(torch_cuda, golden, fb26):
+    """Whole-clip analyser windows: GPU features/labels vs the oracle."""
+    from vad_amd import plan as P
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    pipe = VadPipeline(clf)
+    clip = torch_cuda.from_numpy(w["test_clip"]).cuda()
+    feats = pipe.features(clip).cpu().numpy().astype(np.float64)
+    ref = w["test_x"]
+    nan_rows = np.isnan(ref).any(axis=1)
+    np.testing.assert_array_equal(np.isnan(feats).any(axis=1), nan_rows)
+    labels = pipe.labels(clip).cpu().numpy()
+    ref_l = w["test_labels_ref39"]
+    marg = w["test_margin_ref39"]
+    sure = marg > MARGIN_TOL
+    np.testing.assert_array_equal(labels[sure], ref_l[sure])
+    bad = int((labels != ref_l).sum())
+    assert bad <= max(1, len(ref_l) // 100), bad
+    # same labels from the two-step device path
+    m = pipe.mfcc(clip)
+    np.testing.assert_array_equal(clf.plan.window_labels(m).cpu().numpy(), labels)
+    # offline features on device equal the host-visible process_clip rows
+    off = P.window_features(m, 1).cpu().numpy()
+    assert off.shape == (len(ref_l), 39)
+
+
+def test_labels_short_clips(torch_cuda, golden):
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    w = golden("ffn")
+    pipe = VadPipeline(FFNClassifier(layers_from(w, "ref39", 4)))
+    for L in (0, 400, 1041, 1200, 1201):
+        a = torch_cuda.zeros(max(L, 1), device="cuda")[:L].contiguous()
+        lab = pipe.labels(a)
+        assert lab.numel() == max(O.n_frames(L) - 5, 0)
+
+
+# ---------------------------------------------------------------------------
+# drop-in analyser (feed_frame) traces
+# ---------------------------------------------------------------------------
+def _save_weights(tmp_path, w, b_last=None):
+    from vad_amd.ffn import save_layers
+    p = tmp_path / "ffn.npz"
+    save_layers(str(p), layers_from(w, "ref39", 4, b_last))
+    return str(p)
+
+
+def _replay(an, stream):
+    rets = []
+    for f in stream:
+        r = an.feed_frame(f)
+        rets.append(-1 if r is None else next(i for i, s in enumerate(stream) if s is r))
+    return np.asarray(rets)
+
+
+def test_analyser_trace_matches_reference(torch_cuda, golden, tmp_path):
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    g = golden("analyser")
+    w = golden("ffn")
+    an = SKLearnAnalyzer(_save_weights(tmp_path, w), fft_n=512)
+    an.load_init_inactive_frames(list(g["noise"]))
+    stream = list(g["stream"])
+    rets = _replay(an, stream)
+    ref = g["returns"]
+    # oracle margins of the windows this trace classified
+    marg = O.ffn_margin(g["features"], layers_from(w, "ref39", 4))
+    sure = np.concatenate([np.ones(5, bool), marg > MARGIN_TOL])
+    np.testing.assert_array_equal(rets[sure], ref[sure])
+    assert int((rets != ref).sum()) <= 2
+
+
+def test_analyser_blocks_and_errors(torch_cuda, golden, tmp_path):
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    g = golden("analyser")
+    w = golden("ffn")
+    path = _save_weights(tmp_path, w)
+    an = SKLearnAnalyzer(path)
+    an.load_init_inactive_frames(list(g["noise"]))
+    blocks = list(g["blocks"])  # vad.py's 800-value blocks: truncated to 512
+    np.testing.assert_array_equal(_replay(an, blocks), g["returns_blocks"])
+    # no load_init_inactive_frames -> TypeError on the first feed_frame
+    an2 = SKLearnAnalyzer(path)
+    with pytest.raises(TypeError):
+        an2.feed_frame(g["stream"][0])
+    with pytest.raises(ValueError):
+        an2.load_init_inactive_frames(list(g["noise"][:4]))
+    # MUSIC-capable weights: AssertionError at the same call as the reference
+    an3 = SKLearnAnalyzer(_save_weights(tmp_path, w, w["ref39_b3_music"]))
+    an3.load_init_inactive_frames(list(g["noise"]))
+    k = int(str(g["error_music"]).split(":")[0])
+    stream = list(g["stream"])
+    rets = [an3.feed_frame(f) for f in stream[:k]]
+    ref = g["returns_music"]
+    assert [(-1 if r is None else next(i for i, s in enumerate(stream) if s is r)) for r in rets] \
+        == list(ref)
+    with pytest.raises(AssertionError):
+        an3.feed_frame(stream[k])
+
+
+class _Recorder:
+    """A foreign (non-FFN) classifier: records the rows the analyser passes."""
+
+    def __init__(self, labels):
+        self.labels = list(labels)
+        self.rows = []
+
+    def predict(self, x):
+        self.rows.append(np.array(x))
+        return np.array([self.labels[len(self.rows) - 1]])
+
+
+def test_analyser_foreign_classifier(torch_cuda, golden, tmp_path):
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    g = golden("analyser")
+    ref_rows = g["features"]
+    w = golden("ffn")
+    labels = O.ffn_labels(ref_rows, layers_from(w, "ref39", 4))
+    p = tmp_path / "clf.pkl"
+    with open(p, "wb") as f:
+        pickle.dump(_Recorder(labels), f)
+    an = SKLearnAnalyzer(str(p))
+    an.load_init_inactive_frames(list(g["noise"]))
+    rets = _replay(an, list(g["stream"]))
+    np.testing.assert_array_equal(rets, g["returns"])
+    rows = np.concatenate(an.classifier.rows)
+    assert rows.dtype == np.float64 and rows.shape == ref_rows.shape
+    nan_rows = np.isnan(ref_rows).any(axis=1)
+    np.testing.assert_array_equal(np.isnan(rows).any(axis=1), nan_rows)
+
+
+# ---------------------------------------------------------------------------
+# streaming batch (config 5) == clip path
+# ---------------------------------------------------------------------------
+def test_stream_batch_matches_clip_path(torch_cuda, golden):
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    S, T = 24, 40
+    clips = [O.synth_clip(160 * (T - 1) + 401, seed=600 + s) for s in range(S)]
+    pipe = VadPipeline(clf)
+    want = np.stack([pipe.labels(torch_cuda.from_numpy(c).cuda()).cpu().numpy() for c in clips])
+    for use_graph in (False, True):
+        sb = StreamBatch(S, clf)
+        sb.prime(torch_cuda.from_numpy(np.stack([c[:240] for c in clips])).cuda())
+        if use_graph:
+            sb.capture()
+        got = []
+        for t in range(T):
+            new = np.stack([c[240 + 160 * t: 400 + 160 * t] for c in clips])
+            got.append(sb.step(torch_cuda.from_numpy(new).cuda()).cpu().numpy().copy())
+        got = np.stack(got, axis=1)  # (S, T)
+        assert (got[:, :5] == 255).all()
+        np.testing.assert_array_equal(got[:, 5:], want[:, :T - 5])
+
+
+# ---------------------------------------------------------------------------
+# full-size properties (BASELINE config 3 size)
+# ---------------------------------------------------------------------------
+def test_full_size_properties(torch_cuda, golden):
+    import torch
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    w = golden("ffn")
+    pipe = VadPipeline(FFNClassifier(layers_from(w, "ref39", 4)))
+    F = 1_000_000
+    L = 160 * (F - 1) + 401
+    g = torch.Generator(device="cuda").manual_seed(1)
+    audio = torch.randn(L, device="cuda", generator=g) * 1000.0
+    audio[5_000_000:5_100_000] = 0.0  # a silent stretch
+    lab1 = pipe.labels(audio)
+    lab2 = pipe.labels(audio)
+    assert lab1.numel() == F - 5
+    assert torch.equal(lab1, lab2)                      # deterministic
+    assert int(lab1.max()) <= 2
+    # a segment cut at a frame boundary with a 240-sample + 4-frame halo gives
+    # the same labels as the whole clip (the multi-GPU sharding rule)
+    f0 = 333_333
+    seg = audio[160 * f0: 160 * (f0 + 100_000) + 240 + 160 * 5 + 1].contiguous()
+    lab_seg = pipe.labels(seg)
+    assert torch.equal(lab_seg[:100_000], lab1[f0: f0 + 100_000])
+    # the MFCC of a clip equals the MFCC of its explicit frame matrix
+    m = pipe.mfcc(audio[: 160 * 999 + 401].contiguous())
+    fm = audio[: 160 * 999 + 400].unfold(0, 400, 160).contiguous()
+    m2 = pipe.plan.mfcc(fm)
+    assert torch.equal(m, m2)
+    # labels of silent windows are class 0 (NaN features)
+    c = 5_000_000 // 160 + 10
+    assert int(lab1[c - 2]) == 0

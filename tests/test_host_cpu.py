@@ -1,0 +1,101 @@
+"""CPU-only checks: the C-ABI library loads and exports every symbol the header
+declares, and the host-side logic (filterbank setup, framing, sharding,
+gather) matches the reference fixtures.  No compute call reaches the GPU."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(REPO, "include", "vad_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vad_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    from vad_amd import _lib
+    lib = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 16
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
+
+
+def test_library_is_gfx950():
+    from vad_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_n_frames_matches_reference_framing(golden):
+    from vad_amd import _lib
+    g = golden("clip")
+    lib = _lib.lib()
+    for L, c in zip(g["lens"], g["counts"]):
+        assert lib.vad_n_frames(int(L), 400, 160) == c
+    assert lib.vad_n_frames(160_000_241, 400, 160) == 1_000_000
+    assert lib.vad_n_frames(100, 0, 160) == 0
+
+
+def test_stream_ring_size():
+    from vad_amd import _lib
+    assert _lib.lib().vad_stream_ring_floats(512, 13) == 512 * 5 * 13
+
+
+@pytest.mark.parametrize("name", ["fb_26", "fb_40", "fb_20_0_8000", "fb_32_100_4000"])
+def test_host_filterbank_equals_reference(golden, name):
+    from vad_amd import mfcc
+    g = golden("filterbanks")
+    lo, hi, nf, sr = g[name + "_params"]
+    np.testing.assert_array_equal(mfcc.get_mel_filterbanks(lo, hi, 512, int(nf), sr), g[name])
+    hz = mfcc.hz_from_mel(mfcc.mel_from_hz(lo, hi, int(nf)))
+    np.testing.assert_array_equal(mfcc.convert_to_fft_bins(sr, hz, 512), g[name + "_bins"])
+
+
+def test_split_into_frames(golden):
+    from vad_amd.pipeline import split_into_frames
+    g = golden("clip")
+    for L, c in zip(g["lens"], g["counts"]):
+        fr = split_into_frames(np.arange(int(L)), 400, 160)
+        assert len(fr) == c
+        for i, f in enumerate(fr):
+            assert f[0] == 160 * i and len(f) == 400
+    with pytest.raises(Exception):
+        split_into_frames(np.zeros(10), 4, 2, transcription_path="x.stm")
+
+
+def test_lifter_and_deltas_match_oracle():
+    from oracle import vad_oracle as O
+    from vad_amd import mfcc
+    c = np.random.default_rng(0).standard_normal(13)
+    np.testing.assert_array_equal(mfcc.lifter(c), O.lifter(c))
+    np.testing.assert_array_equal(mfcc.get_deltas(c, c[::-1]), c - c[::-1])
+
+
+def test_shard_range_covers():
+    from vad_amd.dist import shard_range
+    for n in (0, 1, 7, 8, 1000003):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_ffn_layers_roundtrip(tmp_path):
+    from vad_amd.ffn import FFNClassifier, load_layers, random_layers, save_layers, TOPOLOGY_REF39
+    lay = random_layers(TOPOLOGY_REF39, seed=1)
+    p = tmp_path / "w.npz"
+    save_layers(str(p), lay)
+    back = load_layers(str(p))
+    assert len(back) == 4
+    for (w, b), (w2, b2) in zip(lay, back):
+        np.testing.assert_array_equal(w, w2)
+        np.testing.assert_array_equal(b, b2)
+    c = FFNClassifier.load(str(p))
+    assert c.in_dim == 39

@@ -148,3 +148,14 @@ def test_nan_label_is_zero():
     x = np.ones((2, 39))
     x[0, 5] = np.nan
     assert list(O.ffn_labels(x, lay)) == [0, 1]
+
+
+def test_fast_analyser_features_equal_loop(golden):
+    w = golden("ffn")
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    m = O.mfcc_batch(w["test_clip"], fb)
+    a = O.analyser_features(m)
+    b = O.analyser_features_fast(m)
+    np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
+    ok = ~np.isnan(a)
+    assert np.allclose(a[ok], b[ok], rtol=1e-12, atol=1e-12)

@@ -1,0 +1,297 @@
+// extern "C" boundary of libvad_amd.so (include/vad_amd.h): plans, argument
+// checking and kernel dispatch.  Host-side work here is one-off plan setup
+// (filterbank -> sparse taps, lifter x DCT matrix, twiddles, FFN fragments);
+// every hot entry point only validates and launches.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "vad_common.h"
+
+using namespace vad;
+
+struct vad_mfcc_plan {
+  MfccDev host;      // host copy (for introspection)
+  MfccDev* dev;      // device copy read by the kernels
+};
+
+struct vad_ffn_plan {
+  FfnDev net;        // by-value kernel argument, frag -> device buffer
+  float* frag_dev;
+};
+
+#define VAD_TRY(x)                          \
+  do {                                      \
+    hipError_t e_ = (x);                    \
+    if (e_ != hipSuccess) return (int)e_;   \
+  } while (0)
+
+extern "C" {
+
+const char* vad_version(void) { return "vad_amd 0.1 (gfx950)"; }
+
+int64_t vad_n_frames(int64_t n_samples, int32_t frame_size, int32_t hop) {
+  if (frame_size <= 0 || hop <= 0 || n_samples <= frame_size) return 0;
+  return (n_samples - frame_size - 1) / hop + 1;  // while len - offset > frame_size
+}
+
+int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int32_t mfcc_n,
+                         int32_t lifter_L, vad_mfcc_plan** out) {
+  if (!fb || !out || n_filters <= 0 || mfcc_n <= 0) return VAD_EINVAL;
+  if (fft_n != VAD_FFT_N) return VAD_EUNSUPPORTED;
+  if (n_filters > VAD_MAX_FILTERS || mfcc_n > VAD_MAX_MFCC || mfcc_n > n_filters)
+    return VAD_EUNSUPPORTED;
+  vad_mfcc_plan* p = (vad_mfcc_plan*)calloc(1, sizeof(vad_mfcc_plan));
+  if (!p) return VAD_ENOMEM;
+  MfccDev& h = p->host;
+  h.n_filters = n_filters;
+  h.mfcc_n = mfcc_n;
+  // filterbank rows -> contiguous tap ranges [first non-zero, last non-zero]
+  // (NaN counts as non-zero: a degenerate reference filter stays NaN).
+  int off = 0;
+  std::vector<int> cost(n_filters);
+  for (int m = 0; m < n_filters; ++m) {
+    const double* row = fb + (size_t)m * kBins;
+    int lo = -1, hi = -1;
+    for (int k = 0; k < kBins; ++k)
+      if (row[k] != 0.0) { if (lo < 0) lo = k; hi = k; }
+    const int n = lo < 0 ? 0 : hi - lo + 1;
+    if (off + n > VAD_MAX_TAPS) { free(p); return VAD_EUNSUPPORTED; }
+    h.f_lo[m] = lo < 0 ? 0 : lo;
+    h.f_len[m] = n;
+    h.f_off[m] = off;
+    for (int t = 0; t < n; ++t) h.taps[off + t] = (float)row[lo + t];
+    off += n;
+    cost[m] = n + 2 * mfcc_n + 8;  // taps + DCT FMAs + log, in VALU-op units
+  }
+  // balance contiguous filter bands over the 8 waves of phase 2
+  {
+    const int waves = 8;
+    long total = 0;
+    for (int m = 0; m < n_filters; ++m) total += cost[m];
+    int m = 0;
+    long acc = 0;
+    for (int w = 0; w < 16; ++w) { h.wave_fbeg[w] = n_filters; h.wave_fend[w] = n_filters; }
+    for (int w = 0; w < waves; ++w) {
+      h.wave_fbeg[w] = m;
+      const long target = total * (w + 1) / waves;
+      while (m < n_filters && (acc + cost[m] / 2 <= target || w == waves - 1)) acc += cost[m++];
+      h.wave_fend[w] = m;
+    }
+  }
+  // lifter (mfcc.py:85-90) x DCT-II ortho (scipy.fftpack, mfcc.py:76), [c][m]
+  for (int c = 0; c < kMaxCoefs; ++c) {
+    const double lift = lifter_L > 0 ? 1.0 + (lifter_L / 2.0) * sin(M_PI * c / lifter_L) : 1.0;
+    const double sc = c == 0 ? sqrt(1.0 / (4.0 * n_filters)) : sqrt(1.0 / (2.0 * n_filters));
+    for (int m = 0; m < kMaxFilters; ++m) {
+      double v = 0.0;
+      if (c < mfcc_n && m < n_filters)
+        v = lift * sc * 2.0 * cos(M_PI * c * (2.0 * m + 1.0) / (2.0 * n_filters));
+      h.dct[c * kMaxFilters + m] = (float)v;
+    }
+  }
+  for (int n2 = 0; n2 < 16; ++n2)
+    for (int k1 = 0; k1 < 16; ++k1) {
+      const double a = -2.0 * M_PI * n2 * k1 / 256.0;
+      h.tw_a[n2 * 16 + k1] = make_float2((float)cos(a), (float)sin(a));
+    }
+  for (int k = 0; k < 256; ++k) {
+    const double a = -2.0 * M_PI * k / 512.0;
+    h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
+  }
+  hipError_t e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
+  if (e != hipSuccess) { free(p); return (int)e; }
+  e = hipMemcpy(p->dev, &h, sizeof(MfccDev), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->dev); free(p); return (int)e; }
+  *out = p;
+  return VAD_OK;
+}
+
+int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
+  if (!p) return VAD_OK;
+  (void)hipFree(p->dev);
+  free(p);
+  return VAD_OK;
+}
+
+static int check_frames(const vad_mfcc_plan* p, const void* src, int64_t stride, int32_t len,
+                        int64_t n, const void* dst) {
+  if (!p || n < 0) return VAD_EINVAL;
+  if (n == 0) return VAD_OK;
+  if (!src || !dst || stride < 0 || len <= 0) return VAD_EINVAL;
+  return VAD_OK;
+}
+
+int vad_spec_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32_t len, int64_t n,
+                 float* spec, void* stream) {
+  int r = check_frames(p, src, stride, len, n, spec);
+  if (r || n == 0) return r;
+  return (int)launch_mfcc(1, p->dev, src, stride, len, n, spec, (hipStream_t)stream);
+}
+
+int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32_t len, int64_t n,
+                 float* mfcc, void* stream) {
+  int r = check_frames(p, src, stride, len, n, mfcc);
+  if (r || n == 0) return r;
+  return (int)launch_mfcc(0, p->dev, src, stride, len, n, mfcc, (hipStream_t)stream);
+}
+
+int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
+                           void* stream) {
+  int r = check_frames(p, spec, kBins, kBins, n, mfcc);
+  if (r || n == 0) return r;
+  return (int)launch_mfcc(2, p->dev, spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------
+// FFN plan
+// ---------------------------------------------------------------------------
+int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* const* W,
+                        const float* const* b, vad_ffn_plan** out) {
+  if (!dims || !W || !b || !out || n_layers < 1) return VAD_EINVAL;
+  if (n_layers > VAD_MAX_FFN_LAYERS) return VAD_EUNSUPPORTED;
+  for (int l = 0; l <= n_layers; ++l)
+    if (dims[l] <= 0) return VAD_EINVAL;
+  if (dims[0] > 64 || dims[n_layers] > 4) return VAD_EUNSUPPORTED;
+  for (int l = 1; l < n_layers; ++l)
+    if (dims[l] > 64) return VAD_EUNSUPPORTED;
+  for (int l = 0; l < n_layers; ++l)
+    if (!W[l] || !b[l]) return VAD_EINVAL;
+
+  FfnDev net;
+  memset(&net, 0, sizeof(net));
+  net.n_layers = n_layers;
+  for (int l = 0; l <= n_layers; ++l) net.dims[l] = dims[l];
+  net.n_classes = dims[n_layers];
+  // natural shape; the kernels specialise two topologies, everything else
+  // runs on a padded generic shape (ks0 16, 4 tiles per hidden layer)
+  int ks0 = (dims[0] + 3) / 4;
+  int tiles[VAD_MAX_FFN_LAYERS] = {0, 0, 0, 0};
+  for (int l = 0; l < n_layers; ++l) tiles[l] = l + 1 < n_layers ? (dims[l + 1] + 15) / 16 : 1;
+  const bool ref39 = n_layers == 4 && ks0 == 10 && tiles[0] == 4 && tiles[1] == 2 &&
+                     tiles[2] == 1 && tiles[3] == 1;
+  const bool bl13 = n_layers == 3 && ks0 == 4 && tiles[0] == 4 && tiles[1] == 4 && tiles[2] == 1;
+  if (!ref39 && !bl13) {
+    ks0 = 16;
+    for (int l = 0; l < n_layers; ++l) tiles[l] = l + 1 < n_layers ? 4 : 1;
+  }
+  net.ks0 = ks0;
+  for (int l = 0; l < VAD_MAX_FFN_LAYERS; ++l) net.tiles[l] = tiles[l];
+
+  // fragments, in the kernels' slot order
+  auto w_at = [&](int l, int k, int o) -> float {  // W_l[k][o] (Keras (in, out))
+    if (k >= dims[l] || o >= dims[l + 1]) return 0.f;
+    return W[l][(size_t)k * dims[l + 1] + o];
+  };
+  auto b_at = [&](int l, int o) -> float { return o < dims[l + 1] ? b[l][o] : 0.f; };
+  std::vector<float> frag;
+  auto push_slot = [&](auto fn) {
+    for (int lane = 0; lane < 64; ++lane) frag.push_back(fn(lane >> 4, lane & 15));
+  };
+  // layer 0 A: slot mt*ks0 + s -> W0[4s + g][16mt + i]
+  for (int mt = 0; mt < tiles[0]; ++mt)
+    for (int s = 0; s < ks0; ++s)
+      push_slot([&](int g, int i) { return w_at(0, 4 * s + g, 16 * mt + i); });
+  // layer l >= 1 A: slot (mt*TI + t)*4 + r -> W_l[16t + 4g + r][16mt + i]
+  for (int l = 1; l < n_layers; ++l)
+    for (int mt = 0; mt < tiles[l]; ++mt)
+      for (int t = 0; t < tiles[l - 1]; ++t)
+        for (int r = 0; r < 4; ++r)
+          push_slot([&](int g, int i) { return w_at(l, 16 * t + 4 * g + r, 16 * mt + i); });
+  // biases: layer l, slot mt*4 + r -> b_l[16mt + 4g + r]
+  for (int l = 0; l < n_layers; ++l)
+    for (int mt = 0; mt < tiles[l]; ++mt)
+      for (int r = 0; r < 4; ++r) push_slot([&](int g, int) { return b_at(l, 16 * mt + 4 * g + r); });
+
+  vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));
+  if (!p) return VAD_ENOMEM;
+  hipError_t e = hipMalloc((void**)&p->frag_dev, frag.size() * sizeof(float));
+  if (e != hipSuccess) { free(p); return (int)e; }
+  e = hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->frag_dev); free(p); return (int)e; }
+  net.frag = p->frag_dev;
+  p->net = net;
+  *out = p;
+  return VAD_OK;
+}
+
+int vad_ffn_plan_destroy(vad_ffn_plan* p) {
+  if (!p) return VAD_OK;
+  (void)hipFree(p->frag_dev);
+  free(p);
+  return VAD_OK;
+}
+
+int vad_features_f32(const float* mfcc, int64_t n_frames, int32_t mfcc_n, int32_t mode,
+                     float* features, void* stream) {
+  if (n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  const int64_t rows = n_frames > 5 ? n_frames - 5 : 0;
+  if (rows == 0) return VAD_OK;
+  if (!mfcc || !features) return VAD_EINVAL;
+  return (int)launch_features(mfcc, rows, mfcc_n, mode, features, (hipStream_t)stream);
+}
+
+int vad_features_ffn(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frames, int32_t mfcc_n,
+                     int32_t mode, uint8_t* labels, void* stream) {
+  if (!ffn || n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * mfcc_n) return VAD_EINVAL;
+  const int64_t rows = n_frames > 5 ? n_frames - 5 : 0;
+  if (rows == 0) return VAD_OK;
+  if (!mfcc || !labels) return VAD_EINVAL;
+  return (int)launch_ffn(ffn->net, 0, mfcc, rows, mfcc_n, mode, labels, (hipStream_t)stream);
+}
+
+int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t* labels,
+                    void* stream) {
+  if (!ffn || n < 0) return VAD_EINVAL;
+  if (n == 0) return VAD_OK;
+  if (!x || !labels) return VAD_EINVAL;
+  return (int)launch_ffn(ffn->net, 1, x, n, 0, 0, labels, (hipStream_t)stream);
+}
+
+size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, int64_t n_samples,
+                                    int32_t frame_size, int32_t hop) {
+  if (!plan) return 0;
+  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
+  return (size_t)f * plan->host.mfcc_n * sizeof(float);
+}
+
+int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
+                 int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
+                 uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
+  if (f <= 5) return VAD_OK;
+  if (!audio || !labels) return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  const size_t need = vad_mfcc_ffn_workspace_bytes(plan, n_samples, frame_size, hop);
+  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
+  float* mf = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  VAD_TRY(launch_mfcc(0, plan->dev, audio, hop, frame_size, f, mf, st));
+  return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
+}
+
+int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n) {
+  return n_streams * 5 * (int64_t)mfcc_n;
+}
+
+int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
+                    int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
+                    int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream) {
+  if (!plan || !ffn || n_streams < 0 || frame_len <= 0 || frame_stride < 0) return VAD_EINVAL;
+  if (n_streams == 0) return VAD_OK;
+  if (!frames || !ring || !count || !labels || !mfcc_scratch) return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  VAD_TRY(launch_mfcc(0, plan->dev, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
+  return (int)launch_stream_ffn(ffn->net, mfcc_scratch, ring, count, n_streams, plan->host.mfcc_n,
+                                labels, st);
+}
+
+}  // extern "C"

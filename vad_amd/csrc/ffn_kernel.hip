@@ -1,0 +1,327 @@
+// Features (5-frame window, normalisation, deltas) + FFN forward on f32 MFMA.
+//
+// Reference semantics:
+//   features  realtime_analysis/sklearn_analyser.py:52-69,103-107 (analyser,
+//             normalised centre) and dataset/file_processing.py:40-70
+//             (offline, unnormalised);
+//   FFN       learning/ffn_trainer.py:106-116: Dense -> relu (-> relu) ->
+//             Dense -> relu -> ... -> Dense -> softmax; predict = argmax.
+//
+// Layout: one wave classifies a tile of 16 windows with
+// v_mfma_f32_16x16x4_f32 (exact f32: a k-ordered fma chain).  The network
+// runs transposed, H^T = W^T X^T, so a layer's accumulator tile (rows =
+// hidden units 4g + r on lane group g = lane>>4, register r; column = window
+// lane&15) IS the next layer's B operand for K-step (tile, r) -- no lane
+// shuffles between layers.  The W^T A-operand fragments and the bias
+// fragments are laid out per lane on the host ("frag" slots) and held in
+// VGPRs for the whole persistent loop.
+#include "vad_common.h"
+
+namespace vad {
+
+// Feature f of the window whose 5 MFCC rows are r[0..4] (row centre-2+d).
+// Analyser mode normalises the centre by the window mean/std in fp64: the
+// MFCCs are fp32, so the 5-term sums are exact and a constant window gives
+// exactly std = 0 -> 0/0 = NaN, as numpy does on the reference's fp64 rows.
+__device__ __forceinline__ float window_feature(const float* __restrict__ r0,
+                                               const float* __restrict__ r1,
+                                               const float* __restrict__ r2,
+                                               const float* __restrict__ r3,
+                                               const float* __restrict__ r4, int f, int mfcc_n,
+                                               int mode) {
+  const int t = f / mfcc_n;
+  const int c = f - t * mfcc_n;
+  const double a0 = r0[c], a1 = r1[c], a2 = r2[c], a3 = r3[c], a4 = r4[c];
+  if (t == 1) return (float)(a3 - a1);                        // :64 M+1 - M-1
+  double mn = a2;
+  if (mode == VAD_FEAT_ANALYSER) {                            // :103-107
+    const double mean = ((((a0 + a1) + a2) + a3) + a4) / 5.0;
+    const double d0 = a0 - mean, d1 = a1 - mean, d2 = a2 - mean, d3 = a3 - mean, d4 = a4 - mean;
+    const double var = ((((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3) + d4 * d4) / 5.0;
+    mn = d2 / sqrt(var);
+  }
+  if (t == 0) return (float)mn;
+  return (float)((a4 - mn) - (mn - a0));                      // :57-65 second deltas
+}
+
+// argmax of softmax(z) with np.argmax semantics on the fp32 logits: any NaN
+// (or an all-NaN softmax from +inf / all -inf) -> class 0; else first max.
+__device__ __forceinline__ int argmax_classes(const f32x4 z, int n_classes) {
+  bool bad = false;
+  float best = z[0];
+  int arg = 0;
+  bool any_pinf = false, all_ninf = true;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (r < n_classes) {
+      const float v = z[r];
+      bad |= (v != v);
+      any_pinf |= (v == INFINITY);
+      all_ninf &= (v == -INFINITY);
+      if (r > 0 && v > best) { best = v; arg = r; }
+    }
+  }
+  if (bad || any_pinf || all_ninf) return 0;
+  return arg;
+}
+
+// One MFMA layer: out[mt] = bias + sum over (t, r) of A[mt][t*4+r] x in[t][r].
+template <int TO, int TI>
+__device__ __forceinline__ void dense_layer(const float* __restrict__ a, const float* __restrict__ b,
+                                            const f32x4 (&in)[TI], f32x4 (&out)[TO], bool relu) {
+#pragma unroll
+  for (int mt = 0; mt < TO; ++mt) {
+    f32x4 acc = {b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
+#pragma unroll
+    for (int t = 0; t < TI; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(mt * TI + t) * 4 + r], in[t][r], acc, 0, 0, 0);
+    }
+    if (relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = relu_nan(acc[r]);
+    }
+    out[mt] = acc;
+  }
+}
+
+// Network shape: KS0 layer-0 K-steps (4 features each), Tl = 16-row output
+// tiles of layer l (0 = absent).  The last present layer has one tile.
+template <int KS0, int T1, int T2, int T3, int T4>
+struct Topo {
+  static constexpr int NL = (T1 > 0) + (T2 > 0) + (T3 > 0) + (T4 > 0);
+  static constexpr int A0 = T1 * KS0;
+  static constexpr int A1 = T2 * T1 * 4;
+  static constexpr int A2 = T3 * T2 * 4;
+  static constexpr int A3 = T4 * T3 * 4;
+  static constexpr int NA = A0 + A1 + A2 + A3;
+  static constexpr int NB = 4 * (T1 + T2 + T3 + T4);
+};
+
+template <int KS0, int T1, int T2, int T3, int T4>
+__device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const float* __restrict__ fb,
+                                             const float (&x)[KS0]) {
+  using TP = Topo<KS0, T1, T2, T3, T4>;
+  f32x4 h1[T1];
+#pragma unroll
+  for (int mt = 0; mt < T1; ++mt) {
+    f32x4 acc = {fb[mt * 4 + 0], fb[mt * 4 + 1], fb[mt * 4 + 2], fb[mt * 4 + 3]};
+#pragma unroll
+    for (int s = 0; s < KS0; ++s)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[mt * KS0 + s], x[s], acc, 0, 0, 0);
+    if (TP::NL > 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = relu_nan(acc[r]);
+    }
+    h1[mt] = acc;
+  }
+  if constexpr (TP::NL == 1) return h1[0];
+  else {
+    f32x4 h2[T2];
+    dense_layer<T2, T1>(fa + TP::A0, fb + 4 * T1, h1, h2, TP::NL > 2);
+    if constexpr (TP::NL == 2) return h2[0];
+    else {
+      f32x4 h3[T3];
+      dense_layer<T3, T2>(fa + TP::A0 + TP::A1, fb + 4 * (T1 + T2), h2, h3, TP::NL > 3);
+      if constexpr (TP::NL == 3) return h3[0];
+      else {
+        f32x4 h4[T4];
+        dense_layer<T4, T3>(fa + TP::A0 + TP::A1 + TP::A2, fb + 4 * (T1 + T2 + T3), h3, h4, false);
+        return h4[0];
+      }
+    }
+  }
+}
+
+// Source of the layer-0 operands.
+enum Src { kFromMfcc = 0, kFromRows = 1 };
+
+// One wave per 16-window tile, persistent over tiles.
+template <int KS0, int T1, int T2, int T3, int T4, int SRC>
+__global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __restrict__ in,
+                                                  int64_t n_rows, int mfcc_n, int mode,
+                                                  uint8_t* __restrict__ labels) {
+  using TP = Topo<KS0, T1, T2, T3, T4>;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int jw = lane & 15;
+  const int in_dim = net.dims[0];
+
+  float fa[TP::NA];
+  float fb[TP::NB];
+#pragma unroll
+  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
+#pragma unroll
+  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+
+  const int64_t n_tiles = (n_rows + 15) / 16;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t tile = wave_id; tile < n_tiles; tile += n_waves) {
+    const int64_t w = tile * 16 + jw;
+    const bool valid = w < n_rows;
+    float x[KS0];
+#pragma unroll
+    for (int s = 0; s < KS0; ++s) {
+      const int f = 4 * s + g;
+      float v = 0.f;
+      if (f < in_dim && valid) {
+        if constexpr (SRC == kFromMfcc) {
+          const float* r0 = in + w * mfcc_n;
+          v = window_feature(r0, r0 + mfcc_n, r0 + 2 * mfcc_n, r0 + 3 * mfcc_n, r0 + 4 * mfcc_n,
+                             f, mfcc_n, mode);
+        } else {
+          v = in[w * in_dim + f];
+        }
+      }
+      x[s] = v;
+    }
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    if (g == 0 && valid) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+  }
+}
+
+// Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
+// window of each stream is its 5-slot MFCC ring in arrival order
+// (slot (count + d) % 5, oldest first); classify it if count >= 5, then push
+// the new frame's MFCC into the oldest slot (:74 after :71).
+template <int KS0, int T1, int T2, int T3, int T4>
+__global__ __launch_bounds__(256) void stream_ffn_kernel(FfnDev net, const float* __restrict__ newrow,
+                                                         float* __restrict__ ring,
+                                                         int* __restrict__ count, int64_t n_streams,
+                                                         int mfcc_n, uint8_t* __restrict__ labels) {
+  using TP = Topo<KS0, T1, T2, T3, T4>;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int jw = lane & 15;
+  const int in_dim = net.dims[0];
+  float fa[TP::NA];
+  float fb[TP::NB];
+#pragma unroll
+  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
+#pragma unroll
+  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+
+  const int64_t n_tiles = (n_streams + 15) / 16;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t tile = wave_id; tile < n_tiles; tile += n_waves) {
+    const int64_t s = tile * 16 + jw;
+    const bool valid = s < n_streams;
+    const int c = valid ? count[s] : 0;
+    const bool have = valid && c >= 5;
+    float* rs = ring + s * 5 * mfcc_n;
+    float x[KS0];
+#pragma unroll
+    for (int k = 0; k < KS0; ++k) {
+      const int f = 4 * k + g;
+      float v = 0.f;
+      if (have && f < in_dim) {
+        v = window_feature(rs + ((c + 0) % 5) * mfcc_n, rs + ((c + 1) % 5) * mfcc_n,
+                           rs + ((c + 2) % 5) * mfcc_n, rs + ((c + 3) % 5) * mfcc_n,
+                           rs + ((c + 4) % 5) * mfcc_n, f, mfcc_n, VAD_FEAT_ANALYSER);
+      }
+      x[k] = v;
+    }
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    if (valid) {
+      if (g == 0) labels[s] = have ? (uint8_t)argmax_classes(z, net.n_classes) : (uint8_t)255;
+      float* dst = rs + (c % 5) * mfcc_n;
+      for (int cc = g; cc < mfcc_n; cc += 4) dst[cc] = newrow[s * mfcc_n + cc];
+      if (g == 0) count[s] = (c + 1 >= 10) ? c + 1 - 5 : c + 1;
+    }
+  }
+}
+
+// Feature rows only (offline export / tests): one thread per (window, feature).
+__global__ __launch_bounds__(256) void features_kernel(const float* __restrict__ mfcc,
+                                                       int64_t n_rows, int mfcc_n, int mode,
+                                                       float* __restrict__ out) {
+  const int nf = 3 * mfcc_n;
+  const int64_t total = n_rows * nf;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t w = i / nf;
+    const int f = (int)(i - w * nf);
+    const float* r0 = mfcc + w * mfcc_n;
+    out[i] = window_feature(r0, r0 + mfcc_n, r0 + 2 * mfcc_n, r0 + 3 * mfcc_n, r0 + 4 * mfcc_n, f,
+                            mfcc_n, mode);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <int KS0, int T1, int T2, int T3, int T4>
+static hipError_t launch_stream_topo(const FfnDev& net, const float* newrow, float* ring, int* count,
+                                     int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st) {
+  const int64_t n_tiles = (n_streams + 15) / 16;
+  int64_t blocks = (n_tiles + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL((stream_ffn_kernel<KS0, T1, T2, T3, T4>), dim3((int)blocks), dim3(256), 0, st,
+                     net, newrow, ring, count, n_streams, mfcc_n, labels);
+  return hipGetLastError();
+}
+
+template <int KS0, int T1, int T2, int T3, int T4>
+static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64_t n_rows,
+                              int mfcc_n, int mode, uint8_t* labels, hipStream_t st) {
+  const int64_t n_tiles = (n_rows + 15) / 16;
+  int64_t blocks = (n_tiles + 3) / 4;
+  if (blocks > 2048) blocks = 2048;
+  if (src == kFromMfcc)
+    hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, kFromMfcc>), dim3((int)blocks), dim3(256), 0,
+                       st, net, in, n_rows, mfcc_n, mode, labels);
+  else
+    hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, kFromRows>), dim3((int)blocks), dim3(256), 0,
+                       st, net, in, n_rows, mfcc_n, mode, labels);
+  return hipGetLastError();
+}
+
+// Topologies compiled: the reference Keras FFN 39-64-32-16-3
+// (ffn_trainer.py:106-116), BASELINE config 3's 13-64-64-2, and a padded
+// generic shape for anything else within the limits.
+hipError_t launch_ffn(const FfnDev& net, int src, const float* in, int64_t n_rows, int mfcc_n,
+                      int mode, uint8_t* labels, hipStream_t st) {
+  if (n_rows <= 0) return hipSuccess;
+  const int* t = net.tiles;
+  if (net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1)
+    return launch_topo<10, 4, 2, 1, 1>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1)
+    return launch_topo<4, 4, 4, 1, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+  switch (net.n_layers) {
+    case 1: return launch_topo<16, 1, 0, 0, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+    case 2: return launch_topo<16, 4, 1, 0, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+    case 3: return launch_topo<16, 4, 4, 1, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+    default: return launch_topo<16, 4, 4, 4, 1>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+  }
+}
+
+hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring, int* count,
+                             int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st) {
+  if (n_streams <= 0) return hipSuccess;
+  const int* t = net.tiles;
+  if (net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1)
+    return launch_stream_topo<10, 4, 2, 1, 1>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1)
+    return launch_stream_topo<4, 4, 4, 1, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+  switch (net.n_layers) {
+    case 1: return launch_stream_topo<16, 1, 0, 0, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+    case 2: return launch_stream_topo<16, 4, 1, 0, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+    case 3: return launch_stream_topo<16, 4, 4, 1, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+    default: return launch_stream_topo<16, 4, 4, 4, 1>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+  }
+}
+
+hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
+                           hipStream_t st) {
+  if (n_rows <= 0) return hipSuccess;
+  int64_t blocks = (n_rows * 3 * mfcc_n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(features_kernel, dim3((int)blocks), dim3(256), 0, st, mfcc, n_rows, mfcc_n,
+                     mode, out);
+  return hipGetLastError();
+}
+
+}  // namespace vad

@@ -1,0 +1,92 @@
+"""Clip-level (offline / batch) form of the hot path.
+
+Reference call stack: dataset_creator.py -> Pool.map(
+process_file) -> split_into_frames (file_processing.py:80-103) -> per-frame
+get_mfcc -> 5-frame feature window (file_processing.py:40-70), with the
+analyser's classifier applied to every window (sklearn_analyser.py:52-71).
+Here a whole clip resident in HBM is framed, transformed and classified by
+two HIP kernels; the host only sizes buffers.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import MfccConfig
+from .ffn import FFNClassifier
+from .plan import MfccPlan, n_frames, window_features
+
+
+def split_into_frames(data, frame_size, step, transcription_path=None, frame_rate=None):
+    """file_processing.py:80-103 -- list of frame views while len - offset > size."""
+    if transcription_path and frame_rate is None:
+        raise Exception('You must specify frame_rate')
+    if transcription_path:
+        raise NotImplementedError("STM transcript gathering (file_processing.py:87-94) is "
+                                  "outside this build's hot path")
+    frames, offset = [], 0
+    while len(data) - offset > frame_size:
+        frames.append(data[offset:offset + frame_size])
+        offset += step
+    return frames
+
+
+class VadPipeline:
+    """MFCC plan + FFN for whole clips on one GPU.
+
+    mode: "analyser" (normalised centre MFCC, sklearn_analyser.py:52-69) or
+    "offline" (file_processing.py:40-70 features)."""
+
+    def __init__(self, ffn=None, cfg: MfccConfig = MfccConfig(), mode="analyser"):
+        self.cfg = cfg
+        self.plan = MfccPlan.from_config(cfg)
+        if ffn is not None and not isinstance(ffn, FFNClassifier):
+            ffn = FFNClassifier(ffn)
+        self.ffn = ffn
+        self.mode = _lib.FEAT_ANALYSER if mode == "analyser" else _lib.FEAT_OFFLINE
+        self._ws = None
+
+    def n_frames(self, n_samples):
+        return n_frames(n_samples, self.cfg.frame_size, self.cfg.hop)
+
+    def mfcc(self, audio, out=None, stream=None):
+        """(F, n_mfcc) MFCCs of every frame of a device clip."""
+        return self.plan.clip_mfcc(audio, self.cfg.frame_size, self.cfg.hop, out=out, stream=stream)
+
+    def features(self, audio, mode=None, stream=None):
+        """(F-5, 3*n_mfcc) feature rows of a device clip."""
+        m = self.mfcc(audio, stream=stream)
+        return window_features(m, self.mode if mode is None else mode, stream=stream)
+
+    def workspace_bytes(self, n_samples):
+        return int(_lib.lib().vad_mfcc_ffn_workspace_bytes(self.plan.handle, int(n_samples),
+                                                           self.cfg.frame_size, self.cfg.hop))
+
+    def labels(self, audio, out=None, stream=None):
+        """uint8 (F-5,) labels of every window of a device clip (fused path)."""
+        if self.ffn is None:
+            raise ValueError("pipeline has no FFN")
+        if not (isinstance(audio, torch.Tensor) and audio.is_cuda and audio.dtype == torch.float32
+                and audio.is_contiguous()):
+            raise TypeError("audio must be a contiguous float32 CUDA tensor")
+        f = self.n_frames(audio.numel())
+        rows = max(f - 5, 0)
+        if out is None:
+            out = torch.empty((rows,), dtype=torch.uint8, device=audio.device)
+        need = self.workspace_bytes(audio.numel())
+        if need and (self._ws is None or self._ws.numel() < need):
+            self._ws = torch.empty((need,), dtype=torch.uint8, device=audio.device)
+        ws = self._ws
+        _lib.check(_lib.lib().vad_mfcc_ffn(
+            self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.numel(),
+            self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
+            _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), "vad_mfcc_ffn")
+        return out
+
+    def process_clip(self, data):
+        """process_file's feature list for an in-memory clip: (F-5, 3, n_mfcc) float64
+        (unnormalised, file_processing.py:40-70)."""
+        a = torch.from_numpy(np.ascontiguousarray(np.asarray(data).astype(np.float32))).cuda()
+        f = window_features(self.mfcc(a), _lib.FEAT_OFFLINE)
+        return f.cpu().numpy().astype(np.float64).reshape(len(f), 3, -1)

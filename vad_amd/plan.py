@@ -1,0 +1,193 @@
+"""Host objects owning the device plans of libvad_amd (include/vad_amd.h).
+
+``MfccPlan`` holds the filterbank/DCT/twiddle plan of one MFCC configuration
+and runs the HIP MFCC kernel on device tensors; ``FfnPlan`` holds an FFN's
+MFMA fragments.  Both are thin: all arithmetic happens in the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_ptr
+from .config import MfccConfig
+
+
+def _device(dev=None):
+    if dev is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return torch.device(dev)
+
+
+def _require_cuda_tensor(t, name, dtype=torch.float32):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def n_frames(n_samples, frame_size=400, hop=160):
+    """Frames split_into_frames yields (file_processing.py:99: len - offset > size)."""
+    return int(lib().vad_n_frames(int(n_samples), int(frame_size), int(hop)))
+
+
+class MfccPlan:
+    """MFCC plan for a (n_filters, 256) filterbank (mfcc.py:39-56) + mfcc_n + lifter."""
+
+    def __init__(self, filterbank, mfcc_n=13, fft_n=512, lifter_L=22):
+        fb = np.ascontiguousarray(np.asarray(filterbank, dtype=np.float64))
+        if fb.ndim != 2 or fb.shape[1] != fft_n // 2:
+            raise ValueError(f"filterbank must be (n_filters, {fft_n // 2}), got {fb.shape}")
+        self.filterbank = fb
+        self.n_filters = fb.shape[0]
+        self.mfcc_n = int(mfcc_n)
+        self.fft_n = int(fft_n)
+        h = ctypes.c_void_p()
+        check(lib().vad_mfcc_plan_create(fb.ctypes.data_as(ctypes.c_void_p), self.n_filters,
+                                          self.fft_n, self.mfcc_n, int(lifter_L), ctypes.byref(h)),
+              "vad_mfcc_plan_create")
+        self._h = h
+
+    @classmethod
+    def from_config(cls, cfg: MfccConfig = MfccConfig()):
+        from .mfcc import get_mel_filterbanks
+        fb = get_mel_filterbanks(cfg.low_hz, cfg.high_hz, cfg.fft_n, cfg.n_filters, cfg.sample_rate)
+        return cls(fb, cfg.n_mfcc, cfg.fft_n, cfg.lifter)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.vad_mfcc_plan_destroy(h)
+            self._h = None
+
+    # -- frame sources ------------------------------------------------------
+    @staticmethod
+    def _frames_args(src, frame_len, frame_stride, n):
+        _require_cuda_tensor(src, "src")
+        if src.dim() == 2 and frame_len is None:
+            n, frame_len = src.shape
+            frame_stride = frame_len
+        if frame_len is None or frame_stride is None or n is None:
+            raise ValueError("give a (n, frame_len) frame matrix or frame_len/frame_stride/n")
+        if n > 0 and (n - 1) * frame_stride + min(frame_len, 512) > src.numel():
+            raise ValueError("frames run past the end of src")
+        return int(frame_len), int(frame_stride), int(n)
+
+    def spec(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
+        """get_spec_mag (mfcc.py:59-61) of every frame -> (n, 256) fp32."""
+        frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
+        if out is None:
+            out = torch.empty((n, self.fft_n // 2), dtype=torch.float32, device=src.device)
+        check(lib().vad_spec_f32(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
+                                 stream_ptr(stream)), "vad_spec_f32")
+        return out
+
+    def mfcc(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
+        """get_mfcc (mfcc.py:67-69) of every frame -> (n, mfcc_n) fp32."""
+        frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
+        if out is None:
+            out = torch.empty((n, self.mfcc_n), dtype=torch.float32, device=src.device)
+        check(lib().vad_mfcc_f32(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
+                                 stream_ptr(stream)), "vad_mfcc_f32")
+        return out
+
+    def clip_mfcc(self, audio, frame_size=400, hop=160, out=None, stream=None):
+        """MFCC of every frame split_into_frames takes from a clip (file_processing.py:80-103)."""
+        _require_cuda_tensor(audio, "audio")
+        f = n_frames(audio.numel(), frame_size, hop)
+        return self.mfcc(audio, frame_len=frame_size, frame_stride=hop, n=f, out=out, stream=stream)
+
+    def from_spec(self, spec, out=None, stream=None):
+        """get_mfcc_from_spec (mfcc.py:72-78) of (n, 256) spectra -> (n, mfcc_n)."""
+        _require_cuda_tensor(spec, "spec")
+        if spec.dim() != 2 or spec.shape[1] != self.fft_n // 2:
+            raise ValueError("spec must be (n, 256)")
+        n = spec.shape[0]
+        if out is None:
+            out = torch.empty((n, self.mfcc_n), dtype=torch.float32, device=spec.device)
+        check(lib().vad_mfcc_from_spec_f32(self._h, ptr(spec), n, ptr(out), stream_ptr(stream)),
+              "vad_mfcc_from_spec_f32")
+        return out
+
+
+class FfnPlan:
+    """Device fragments of a Keras-style MLP (ffn_trainer.py:106-116)."""
+
+    def __init__(self, layers):
+        self.layers = [(np.ascontiguousarray(np.asarray(w, np.float32)),
+                        np.ascontiguousarray(np.asarray(b, np.float32)).reshape(-1))
+                       for w, b in layers]
+        dims = [self.layers[0][0].shape[0]] + [w.shape[1] for w, _ in self.layers]
+        for (w, b), i, o in zip(self.layers, dims[:-1], dims[1:]):
+            if w.shape != (i, o) or b.shape != (o,):
+                raise ValueError(f"layer shapes do not chain: W {w.shape}, b {b.shape}")
+        self.dims = dims
+        n = len(self.layers)
+        d = (ctypes.c_int32 * (n + 1))(*dims)
+        wp = (ctypes.c_void_p * n)(*[w.ctypes.data for w, _ in self.layers])
+        bp = (ctypes.c_void_p * n)(*[b.ctypes.data for _, b in self.layers])
+        h = ctypes.c_void_p()
+        check(lib().vad_ffn_plan_create(n, d, wp, bp, ctypes.byref(h)), "vad_ffn_plan_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def in_dim(self):
+        return self.dims[0]
+
+    @property
+    def n_classes(self):
+        return self.dims[-1]
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib._lib is not None:
+            _lib._lib.vad_ffn_plan_destroy(h)
+            self._h = None
+
+    def predict(self, x, out=None, stream=None):
+        """Labels (uint8) of feature rows x (n, in_dim) fp32 on the device."""
+        _require_cuda_tensor(x, "x")
+        if x.dim() != 2 or x.shape[1] != self.in_dim:
+            raise ValueError(f"x must be (n, {self.in_dim})")
+        n = x.shape[0]
+        if out is None:
+            out = torch.empty((n,), dtype=torch.uint8, device=x.device)
+        check(lib().vad_ffn_predict(self._h, ptr(x), n, ptr(out), stream_ptr(stream)),
+              "vad_ffn_predict")
+        return out
+
+    def window_labels(self, mfcc, mode=_lib.FEAT_ANALYSER, out=None, stream=None):
+        """Labels of every 5-frame window of an MFCC sequence (F-5 rows)."""
+        _require_cuda_tensor(mfcc, "mfcc")
+        f, c = mfcc.shape
+        rows = max(f - 5, 0)
+        if out is None:
+            out = torch.empty((rows,), dtype=torch.uint8, device=mfcc.device)
+        check(lib().vad_features_ffn(self._h, ptr(mfcc), f, c, int(mode), ptr(out),
+                                     stream_ptr(stream)), "vad_features_ffn")
+        return out
+
+
+def window_features(mfcc, mode=_lib.FEAT_ANALYSER, out=None, stream=None):
+    """(F-5, 3*n) feature rows of an (F, n) MFCC sequence (analyser or offline form)."""
+    _require_cuda_tensor(mfcc, "mfcc")
+    f, c = mfcc.shape
+    rows = max(f - 5, 0)
+    if out is None:
+        out = torch.empty((rows, 3 * c), dtype=torch.float32, device=mfcc.device)
+    check(lib().vad_features_f32(ptr(mfcc), f, c, int(mode), ptr(out), stream_ptr(stream)),
+          "vad_features_f32")
+    return out
