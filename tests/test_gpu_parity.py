@@ -172,7 +172,7 @@ def test_ffn_generic_topology(torch_cuda):
     """A shape outside the specialised ones runs on the padded generic kernel."""
     from vad_amd.ffn import FFNClassifier, random_layers
     rng = np.random.default_rng(4)
-    for dims in ((20, 48, 3), (39, 10), (7, 33, 17, 5, 4)):
+    for dims in ((20, 48, 3), (39, 4), (7, 33, 17, 5, 4), (64, 64, 64, 64, 2)):
         lay = random_layers(dims, seed=len(dims))
         x = rng.standard_normal((333, dims[0])) * 2
         ref = O.ffn_labels(x.astype(np.float32), lay)
