@@ -37,98 +37,144 @@ constexpr int kPStride = kBins + 1;             // floats per P row (bank pad)
 enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 
 // Load z[16 n1 + n2] = (x[32 n1 + 2 n2], x[32 n1 + 2 n2 + 1]), n1 < NZ.
-template <int NZ, bool VEC2>
-__device__ __forceinline__ void load_stage_a(const float* __restrict__ fr, int len, int n2,
-                                             float2 (&u)[16]) {
+// Branch-free and wait-free: every load is issued unconditionally from an
+// address clamped into the frame, so all NZ loads of a pass are in flight
+// at once; the zero padding (x[t] = 0 for t >= len) is applied later by
+// pad_stage_a, at first use.  LEN > 0 fixes the frame length at compile time
+// (400 for clips); VEC2 (8-byte aligned frames of even length) loads float2.
+template <int NZ, bool VEC2, int LEN>
+__device__ __forceinline__ void load_stage_a(const float* __restrict__ fr, int len_rt, int n2,
+                                             float2 (&u)[NZ]) {
+  const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
   for (int n1 = 0; n1 < NZ; ++n1) {
     const int t = 32 * n1 + 2 * n2;
     if constexpr (VEC2) {
-      if (t + 1 < len) {
-        u[n1] = *reinterpret_cast<const float2*>(fr + t);
-      } else {
-        u[n1] = make_float2(t < len ? fr[t] : 0.f, 0.f);
-      }
+      const int tc = t < len - 2 ? t : len - 2;
+      u[n1] = *reinterpret_cast<const float2*>(fr + tc);
     } else {
-      u[n1] = make_float2(t < len ? fr[t] : 0.f, t + 1 < len ? fr[t + 1] : 0.f);
+      const int t0 = t < len - 1 ? t : len - 1;
+      const int t1 = t + 1 < len - 1 ? t + 1 : len - 1;
+      u[n1] = make_float2(fr[t0], fr[t1]);
     }
   }
 }
 
-// Phase 1 for one frame group: power spectrum of frame `fr` into P (LDS row
-// or global row, stride 1).  j = lane within the 16-lane group.
-template <int NZ, bool VEC2>
-__device__ __forceinline__ void frame_power(const MfccDev* __restrict__ plan,
-                                            const float* __restrict__ fr, int len, bool valid,
-                                            int j, float2* __restrict__ scr,
-                                            float* __restrict__ prow) {
-  // ---- stage A: DFT16 over n1 for n2 = j -------------------------------
-  float2 u[16];
-  if (valid) {
-    load_stage_a<NZ, VEC2>(fr, len, j, u);
-  } else {
+template <int NZ, int LEN>
+__device__ __forceinline__ void pad_stage_a(int len_rt, int n2, float2 (&u)[NZ]) {
+  const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
-    for (int n = 0; n < NZ; ++n) u[n] = make_float2(0.f, 0.f);
+  for (int n1 = 0; n1 < NZ; ++n1) {
+    if (LEN > 0 && 32 * n1 + 31 < LEN) continue;  // every lane in range (compile time)
+    const int t = 32 * n1 + 2 * n2;
+    u[n1].x = t < len ? u[n1].x : 0.f;
+    u[n1].y = t + 1 < len ? u[n1].y : 0.f;
   }
+}
+
+// Per-lane constants of a 16-lane FFT group, loaded once per workgroup.
+//   stage B: lane j owns the even half of column cE and the odd half of
+//   column cO = 16 - cE (lanes 0..13 cover columns 1..7 / 9..15, lane 14
+//   column 0, lane 15 column 8); the pair m = (a_m, b_m) of the real-FFT
+//   split is (E[m], O[7-m]) = (Z[k], Z[256-k]) with k = cE + 32 m.
+//   Column 0 pairs k2 with -k2 (mod 16) instead, so lane 14 permutes its
+//   registers into (Z[16 m], Z[256 - 16 m]) pairs; its m = 0 pair holds the
+//   two self-partnered bins 0 and 128, fixed up explicitly.
+struct LaneConsts {
+  float2 twa[16];  // W256^(j k1)
+  float2 twb[8];   // W512^kE(m)
+  int cE, cO;
+  int e0, es;      // kE(m) = e0 + es*m
+  int o0;          // kO(m) = o0 - es*m (m >= 1)
+  int kO0;         // kO(0)
+  bool col0;
+};
+
+__device__ __forceinline__ void lane_consts(const MfccDev* __restrict__ plan, int j, LaneConsts& L) {
+  if (j < 14) {
+    const int p = (j >> 1) + 1;
+    L.cE = (j & 1) ? 16 - p : p;
+    L.cO = 16 - L.cE;
+  } else {
+    L.cE = L.cO = (j == 14) ? 0 : 8;
+  }
+  L.col0 = (j == 14);
+  L.e0 = L.cE;
+  L.es = L.col0 ? 16 : 32;
+  L.o0 = 256 - L.cE;
+  L.kO0 = L.col0 ? 128 : 256 - L.cE;
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) L.twa[k1] = plan->tw_a[j * 16 + k1];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) L.twb[m] = plan->tw_b[L.e0 + L.es * m];
+}
+
+// Phase 1 for one frame of a 16-lane group: power spectrum into prow
+// (LDS row, or a global row in spectrum mode).  SCALE multiplies |2X|^2 into
+// P = |X/512|^2 (2^-20); the MFCC modes fold that factor into the mel taps.
+template <int NZ, int LEN, bool SCALE>
+__device__ __forceinline__ void frame_power(float2 (&u_in)[NZ], int len, const LaneConsts& L, int j,
+                                            float2* __restrict__ scr, float* __restrict__ prow) {
+  // ---- stage A: DFT16 over n1 for n2 = j, twiddle W256^(j k1), to LDS ----
+  pad_stage_a<NZ, LEN>(len, j, u_in);
+  float2 u[16];
+#pragma unroll
+  for (int n = 0; n < NZ; ++n) u[n] = u_in[n];
   dft16<NZ>(u);
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) u[k1] = cmul(u[k1], plan->tw_a[j * 16 + k1]);
+  for (int k1 = 1; k1 < 16; ++k1) u[k1] = cmul(u[k1], L.twa[k1]);
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) scr[k1 * kColStride + j] = u[k1];
   __builtin_amdgcn_wave_barrier();
 
   // ---- stage B: even half of column cE, odd half of column cO ----------
-  int cE, cO;
-  if (j < 14) {
-    const int p = (j >> 1) + 1;
-    cE = (j & 1) ? 16 - p : p;
-    cO = 16 - cE;
-  } else {
-    cE = cO = (j == 14) ? 0 : 8;
-  }
   float2 E[8], O[8];
   {
     float2 col[16];
 #pragma unroll
-    for (int n = 0; n < 16; ++n) col[n] = scr[cE * kColStride + n];
+    for (int n = 0; n < 16; ++n) col[n] = scr[L.cE * kColStride + n];
     dft16_even(col, E);  // E[m] = Z[cE + 32 m]
 #pragma unroll
-    for (int n = 0; n < 16; ++n) col[n] = scr[cO * kColStride + n];
+    for (int n = 0; n < 16; ++n) col[n] = scr[L.cO * kColStride + n];
     dft16_odd(col, O);   // O[m] = Z[cO + 32 m + 16]
   }
   __builtin_amdgcn_wave_barrier();
 
-  // ---- real-FFT split: X[k] = (S - i W^k D)/2, S = a + conj(b), D = a - conj(b)
-  const bool col0 = (j == 14);
+  // ---- real-FFT split on pairs (a, b) = (Z[k], Z[256-k]):
+  //   2 X[k] = S - i W^k D,  2 X[256-k] = conj(S) - i conj(W^k D),
+  //   S = a + conj(b), D = a - conj(b),  W = W512
+  // column-0 lane: E' = (Z0, Z16, ..., Z112), O'[7-m] = Z[256 - 16 m]
+  const float2 Ep[8] = {E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3]};
+  const float2 Op[8] = {O[4], E[5], O[5], E[6], O[6], E[7], O[7], E[4]};
+  constexpr float sc = SCALE ? 0x1p-20f : 1.0f;
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    {  // slot E[m], bin k = cE + 32 m, partner Z[256 - k]
-      const int k = cE + 32 * m;
-      const float2 a = E[m];
-      const float2 b0 = O[7 - m], b1 = E[(8 - m) & 7];
-      const float2 b = make_float2(col0 ? b1.x : b0.x, col0 ? b1.y : b0.y);
-      const float2 S = make_float2(a.x + b.x, a.y - b.y);
-      const float2 D = make_float2(a.x - b.x, a.y + b.y);
-      const float2 T = cmul(D, plan->tw_b[k]);
-      const float xr = S.x + T.y, xi = S.y - T.x;
-      prow[k] = fmaf(xr, xr, xi * xi) * 0x1p-20f;
+    const float2 a = make_float2(L.col0 ? Ep[m].x : E[m].x, L.col0 ? Ep[m].y : E[m].y);
+    const float2 b = make_float2(L.col0 ? Op[7 - m].x : O[7 - m].x,
+                                 L.col0 ? Op[7 - m].y : O[7 - m].y);
+    const float2 S = make_float2(a.x + b.x, a.y - b.y);
+    const float2 D = make_float2(a.x - b.x, a.y + b.y);
+    const float2 T = cmul(D, L.twb[m]);
+    const float xr = S.x + T.y, xi = S.y - T.x;        // 2 X[k]
+    const float yr = S.x - T.y, yi = -S.y - T.x;       // 2 X[256-k]
+    float pk = fmaf(xr, xr, xi * xi) * sc;
+    float pn = fmaf(yr, yr, yi * yi) * sc;
+    if (m == 0) {  // lane 14: bins 0 and 128 are their own partners
+      const float s0 = a.x + a.y;                       // X[0] = Re Z0 + Im Z0
+      const float p0 = 4.f * s0 * s0 * sc;
+      const float p128 = 4.f * fmaf(b.x, b.x, b.y * b.y) * sc;  // X[128] = conj(Z128)
+      pk = L.col0 ? p0 : pk;
+      pn = L.col0 ? p128 : pn;
     }
-    {  // slot O[m], bin k = cO + 32 m + 16
-      const int k = cO + 32 * m + 16;
-      const float2 a = O[m];
-      const float2 b0 = E[7 - m], b1 = O[7 - m];
-      const float2 b = make_float2(col0 ? b1.x : b0.x, col0 ? b1.y : b0.y);
-      const float2 S = make_float2(a.x + b.x, a.y - b.y);
-      const float2 D = make_float2(a.x - b.x, a.y + b.y);
-      const float2 T = cmul(D, plan->tw_b[k]);
-      const float xr = S.x + T.y, xi = S.y - T.x;
-      prow[k] = fmaf(xr, xr, xi * xi) * 0x1p-20f;
-    }
+    const int kE = L.e0 + L.es * m;
+    const int kO = m == 0 ? L.kO0 : L.o0 - L.es * m;
+    prow[kE] = pk;
+    prow[kO] = pn;
   }
 }
 
-// Phase 2: frame `lane` of the tile, filters [fb, fe): returns partial
-// lifter x DCT sums in acc[].
+// Phase 2: frame `lane` of the tile, filters [fb, fe): partial lifter x DCT
+// sums in acc[].
 __device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
                                             const float* __restrict__ prow, int fb, int fe,
                                             float (&acc)[kMaxCoefs]) {
@@ -138,14 +184,17 @@ __device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
   for (int m = fb; m < fe; ++m) {
     const int lo = plan->f_lo[m], n = plan->f_len[m];
     const float* w = plan->taps + plan->f_off[m];
-    float e0 = 0.f, e1 = 0.f;
+    const float* pr = prow + lo;
+    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
     int t = 0;
-    for (; t + 1 < n; t += 2) {
-      e0 = fmaf(w[t], prow[lo + t], e0);
-      e1 = fmaf(w[t + 1], prow[lo + t + 1], e1);
+    for (; t + 3 < n; t += 4) {
+      e0 = fmaf(w[t], pr[t], e0);
+      e1 = fmaf(w[t + 1], pr[t + 1], e1);
+      e2 = fmaf(w[t + 2], pr[t + 2], e2);
+      e3 = fmaf(w[t + 3], pr[t + 3], e3);
     }
-    if (t < n) e0 = fmaf(w[t], prow[lo + t], e0);
-    float e = e0 + e1;
+    for (; t < n; ++t) e0 = fmaf(w[t], pr[t], e0);
+    float e = (e0 + e1) + (e2 + e3);
     e = (e == 0.f) ? eps : e;
     const float lg = __log10f(e);
 #pragma unroll
@@ -153,65 +202,111 @@ __device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
   }
 }
 
-template <int MODE, int NZ, bool VEC2>
+constexpr int kPartStride = kMaxCoefs + 1;  // floats per (wave, frame) partial row
+
+// Phases 2 + 3 for one tile: mel / log / DCT partials per wave, summed
+// through LDS, coalesced store of the tile's MFCC rows.
+__device__ __forceinline__ void tile_mfcc(const MfccDev* __restrict__ plan, const float* P,
+                                          float* part, int tid, int wave, int lane, int64_t f0,
+                                          int64_t n_frames, int mfcc_n, float* __restrict__ out) {
+  __syncthreads();
+  float acc[kMaxCoefs];
+  mel_log_dct(plan, P + lane * kPStride, plan->wave_fbeg[wave], plan->wave_fend[wave], acc);
+#pragma unroll
+  for (int c = 0; c < kMaxCoefs; ++c) part[(wave * 64 + lane) * kPartStride + c] = acc[c];
+  __syncthreads();
+  const int64_t nf = (n_frames - f0) < kTile ? (n_frames - f0) : kTile;
+  for (int i = tid; i < nf * mfcc_n; i += kThreads) {
+    const int lf = i / mfcc_n, c = i - lf * mfcc_n;
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += part[(w * 64 + lf) * kPartStride + c];
+    out[f0 * mfcc_n + i] = s;
+  }
+  __syncthreads();
+}
+
+template <int MODE, int NZ, bool VEC2, int LEN>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* P = reinterpret_cast<float*>(smem);                                   // [64][257]
   float2* scr = reinterpret_cast<float2*>(smem + kTile * kPStride * sizeof(float));
-  float* part = reinterpret_cast<float*>(scr);                                 // phase 3 reuse
+  float* part = reinterpret_cast<float*>(scr);            // phase 3 reuse: [wave][64][17]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  // wave-uniform (SGPR): the plan reads in phase 2 become scalar loads that
+  // do not queue behind the prefetched samples on vmcnt
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = tid >> 4;  // frame group 0..31
   const int j = tid & 15;
   const int len = frame_len < kFftN ? frame_len : kFftN;
   const int mfcc_n = plan->mfcc_n;
   const int64_t n_tiles = (n_frames + kTile - 1) / kTile;
 
-  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    const int64_t f0 = tile * kTile;
-    if constexpr (MODE == kSpecToMfcc) {
-      // stage the tile's spectra into P (coalesced rows)
+  if constexpr (MODE == kSpecToMfcc) {
+    for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+      const int64_t f0 = tile * kTile;
       for (int i = tid; i < kTile * kBins; i += kThreads) {
         const int lf = i / kBins, k = i - lf * kBins;
         const int64_t f = f0 + lf;
-        P[lf * kPStride + k] = (f < n_frames) ? src[f * kBins + k] : 0.f;
+        // the taps carry the FFT path's 2^-20: undo it on true spectra (exact)
+        P[lf * kPStride + k] = (f < n_frames) ? src[f * kBins + k] * 0x1p20f : 0.f;
       }
-    } else {
-#pragma unroll 1
-      for (int pass = 0; pass < kTile / kGroups; ++pass) {
-        const int lf = pass * kGroups + grp;
-        const int64_t f = f0 + lf;
-        const bool valid = f < n_frames;
-        const float* fr = src + (valid ? f : 0) * frame_stride;
+      tile_mfcc(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
+    }
+  } else {
+    float2* gscr = scr + grp * kGroupScratch;
+    LaneConsts L;
+    lane_consts(plan, j, L);
+    // software pipeline: the samples of the next pass are in flight while
+    // the current pass computes
+    float2 bufA[NZ], bufB[NZ];
+    const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
+    int64_t tile = blockIdx.x;
+    {
+      int64_t f = tile * kTile + grp;
+      f = f < flast ? f : flast;
+      load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
+    }
+    for (; tile < n_tiles; tile += gridDim.x) {
+      const int64_t f0 = tile * kTile;
+      {  // prefetch pass 1 of this tile
+        int64_t f = f0 + kGroups + grp;
+        f = f < flast ? f : flast;
+        load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufB);
+      }
+      // keep the scheduler from hoisting the next pass's FFT above this
+      // pass (that would wait on the loads just issued and defeat the
+      // prefetch distance)
+      __builtin_amdgcn_sched_barrier(0);
+      {  // pass 0
+        const int64_t f = f0 + grp;
         if constexpr (MODE == kAudioToSpec) {
-          float* prow = out + (valid ? f : 0) * kBins;
-          if (valid) frame_power<NZ, VEC2>(plan, fr, len, valid, j, scr + grp * kGroupScratch, prow);
+          if (f < n_frames) frame_power<NZ, LEN, true>(bufA, len, L, j, gscr, out + f * kBins);
         } else {
-          frame_power<NZ, VEC2>(plan, fr, len, valid, j, scr + grp * kGroupScratch,
-                                P + lf * kPStride);
+          frame_power<NZ, LEN, false>(bufA, len, L, j, gscr, P + grp * kPStride);
         }
       }
-    }
-    if constexpr (MODE != kAudioToSpec) {
-      __syncthreads();
-      float acc[kMaxCoefs];
-      mel_log_dct(plan, P + lane * kPStride, plan->wave_fbeg[wave], plan->wave_fend[wave], acc);
-      // part[wave][c][lane]
-      for (int c = 0; c < mfcc_n; ++c) part[(wave * kMaxCoefs + c) * 64 + lane] = acc[c];
-      __syncthreads();
-      const int64_t nf = (n_frames - f0) < kTile ? (n_frames - f0) : kTile;
-      for (int i = tid; i < nf * mfcc_n; i += kThreads) {
-        const int lf = i / mfcc_n, c = i - lf * mfcc_n;
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < kWaves; ++w) s += part[(w * kMaxCoefs + c) * 64 + lf];
-        out[f0 * mfcc_n + i] = s;
+      __builtin_amdgcn_sched_barrier(0);
+      {  // prefetch pass 0 of the next tile
+        int64_t f = (tile + gridDim.x) * kTile + grp;
+        f = f < flast ? f : flast;
+        load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
       }
-      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      {  // pass 1
+        const int64_t f = f0 + kGroups + grp;
+        if constexpr (MODE == kAudioToSpec) {
+          if (f < n_frames) frame_power<NZ, LEN, true>(bufB, len, L, j, gscr, out + f * kBins);
+        } else {
+          frame_power<NZ, LEN, false>(bufB, len, L, j, gscr, P + (kGroups + grp) * kPStride);
+        }
+      }
+      if constexpr (MODE == kAudioToMfcc)
+        tile_mfcc(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -219,24 +314,36 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
 size_t mfcc_smem_bytes() {
   const size_t p = kTile * kPStride * sizeof(float);  // 65792 B, 16-B multiple
   const size_t s = kGroups * kGroupScratch * sizeof(float2);
-  const size_t part = kWaves * kMaxCoefs * 64 * sizeof(float);
+  const size_t part = kWaves * 64 * kPartStride * sizeof(float);
   return p + (s > part ? s : part);
 }
 
-template <int MODE, int NZ, bool VEC2>
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int MODE, int NZ, bool VEC2, int LEN = 0>
 static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int grid = (int)(n_tiles < 4096 ? n_tiles : 4096);
+  const int cap = num_cus();  // persistent: one 512-thread workgroup per CU (LDS-bound)
+  const int grid = (int)(n_tiles < cap ? n_tiles : cap);
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2>), dim3(grid), dim3(kThreads), smem, st, plan,
+  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN>), dim3(grid), dim3(kThreads), smem, st, plan,
                      src, stride, len, n, out);
   return hipGetLastError();
 }
@@ -245,7 +352,10 @@ template <int MODE>
 static hipError_t launch_m(const MfccDev* plan, const float* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int used = len < kFftN ? len : kFftN;
-  const bool vec2 = ((reinterpret_cast<uintptr_t>(src) & 7) == 0) && ((stride & 1) == 0);
+  const bool vec2 = ((reinterpret_cast<uintptr_t>(src) & 7) == 0) && ((stride & 1) == 0) &&
+                    ((used & 1) == 0);
+  if (used == 400 && vec2)  // the reference framing (config.py:21): fully specialised
+    return launch_t<MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
   if (used <= 32 * 13) {
     return vec2 ? launch_t<MODE, 13, true>(plan, src, stride, len, n, out, st)
                 : launch_t<MODE, 13, false>(plan, src, stride, len, n, out, st);
@@ -260,7 +370,7 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, const float* src, int64_t 
   switch (mode) {
     case kAudioToMfcc: return launch_m<kAudioToMfcc>(plan, src, stride, len, n, out, st);
     case kAudioToSpec: return launch_m<kAudioToSpec>(plan, src, stride, len, n, out, st);
-    default: return launch_t<kSpecToMfcc, 13, false>(plan, src, 0, 0, n, out, st);
+    default: return launch_t<kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
   }
 }
 
