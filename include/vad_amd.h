@@ -59,6 +59,13 @@ int vad_mfcc_plan_create(const double* filterbank_host, int32_t n_filters, int32
                          int32_t mfcc_n, int32_t lifter_L, vad_mfcc_plan** out);
 int vad_mfcc_plan_destroy(vad_mfcc_plan* plan);
 
+/* Kernel variant a plan dispatches to: 0 = runtime filterbank tables,
+ * 1 / 2 = the compile-time tables of the reference's 26 / 40-filter banks
+ * (selected only when the plan equals them bit for bit).  set_variant(0)
+ * forces the runtime path (tests compare the two). */
+int32_t vad_mfcc_plan_variant(const vad_mfcc_plan* plan);
+int vad_mfcc_plan_set_variant(vad_mfcc_plan* plan, int32_t variant);
+
 /* Frames f = 0..n_frames-1 start at src + f*frame_stride and hold frame_len
  * samples (fp32); only the first min(frame_len, 512) feed the 512-point FFT
  * (np.fft.fft(x, 512) zero-pads / truncates, mfcc.py:61).

@@ -374,3 +374,23 @@ def test_full_size_properties(torch_cuda, golden):
     # labels of silent windows are class 0 (NaN features)
     c = 5_000_000 // 160 + 10
     assert int(lab1[c - 2]) == 0
+
+
+@pytest.mark.parametrize("nf", [26, 40])
+def test_compiled_tables_match_runtime_path(torch_cuda, golden, nf):
+    """The compile-time Mel26/Mel40 kernels and the runtime-table kernel agree."""
+    from vad_amd.plan import MfccPlan
+    fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+    p = MfccPlan(fb)
+    assert p.variant == (1 if nf == 26 else 2)
+    clip = torch_cuda.from_numpy(O.synth_clip(160 * 2000 + 401, seed=9)).cuda()
+    m_spec = p.clip_mfcc(clip).cpu().numpy()
+    p.set_variant(0)
+    assert p.variant == 0
+    m_gen = p.clip_mfcc(clip).cpu().numpy()
+    assert frame_rel(m_spec, m_gen).max() <= 1e-5
+    ref = O.mfcc_batch(clip.cpu().numpy(), fb)
+    assert_mfcc_close(m_spec, ref)
+    assert_mfcc_close(m_gen, ref)
+    # a non-reference bank stays on the runtime path
+    assert MfccPlan(O.get_mel_filterbanks(100, 4000, 512, 32, 16000)).variant == 0

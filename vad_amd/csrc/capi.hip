@@ -9,13 +9,33 @@
 #include <vector>
 
 #include "vad_common.h"
+#include "mel_tables.h"
 
 using namespace vad;
 
 struct vad_mfcc_plan {
   MfccDev host;      // host copy (for introspection)
   MfccDev* dev;      // device copy read by the kernels
+  int spec;          // 1/2: equals the compile-time Mel26/Mel40 tables bit for bit
 };
+
+// Does the runtime plan equal compile-time table T (taps, ranges, DCT rows)?
+template <class T>
+static bool matches_table(const MfccDev& h) {
+  if (h.n_filters != T::NF || h.mfcc_n != T::NC) return false;
+  for (int m = 0; m < T::NF; ++m) {
+    if (h.f_lo[m] != T::lo[m] || h.f_len[m] != T::len[m]) return false;
+    for (int k = 0; k < kBins; ++k) {
+      const bool in = k >= T::lo[m] && k < T::lo[m] + T::len[m];
+      const float v = in ? h.taps[h.f_off[m] + k - T::lo[m]] : 0.f;
+      if (memcmp(&v, &T::w[m][k], sizeof(float)) != 0) return false;
+    }
+  }
+  for (int c = 0; c < T::NC; ++c)
+    for (int m = 0; m < T::NF; ++m)
+      if (memcmp(&h.dct[c * kMaxFilters + m], &T::dct[c][m], sizeof(float)) != 0) return false;
+  return true;
+}
 
 struct vad_ffn_plan {
   FfnDev net;        // by-value kernel argument, frag -> device buffer
@@ -102,6 +122,7 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     const double a = -2.0 * M_PI * k / 512.0;
     h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
   }
+  p->spec = matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
   hipError_t e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
   if (e != hipSuccess) { free(p); return (int)e; }
   e = hipMemcpy(p->dev, &h, sizeof(MfccDev), hipMemcpyHostToDevice);
@@ -117,6 +138,16 @@ int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
   return VAD_OK;
 }
 
+int32_t vad_mfcc_plan_variant(const vad_mfcc_plan* p) { return p ? p->spec : -1; }
+
+int vad_mfcc_plan_set_variant(vad_mfcc_plan* p, int32_t variant) {
+  if (!p) return VAD_EINVAL;
+  if (variant == 0) { p->spec = 0; return VAD_OK; }
+  if (variant == 1 && matches_table<Mel26>(p->host)) { p->spec = 1; return VAD_OK; }
+  if (variant == 2 && matches_table<Mel40>(p->host)) { p->spec = 2; return VAD_OK; }
+  return VAD_EINVAL;
+}
+
 static int check_frames(const vad_mfcc_plan* p, const void* src, int64_t stride, int32_t len,
                         int64_t n, const void* dst) {
   if (!p || n < 0) return VAD_EINVAL;
@@ -129,21 +160,21 @@ int vad_spec_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
                  float* spec, void* stream) {
   int r = check_frames(p, src, stride, len, n, spec);
   if (r || n == 0) return r;
-  return (int)launch_mfcc(1, p->dev, src, stride, len, n, spec, (hipStream_t)stream);
+  return (int)launch_mfcc(1, p->dev, 0, src, stride, len, n, spec, (hipStream_t)stream);
 }
 
 int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32_t len, int64_t n,
                  float* mfcc, void* stream) {
   int r = check_frames(p, src, stride, len, n, mfcc);
   if (r || n == 0) return r;
-  return (int)launch_mfcc(0, p->dev, src, stride, len, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
                            void* stream) {
   int r = check_frames(p, spec, kBins, kBins, n, mfcc);
   if (r || n == 0) return r;
-  return (int)launch_mfcc(2, p->dev, spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc(2, p->dev, p->spec, spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -274,7 +305,7 @@ int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float
   if (!workspace || workspace_bytes < need) return VAD_EINVAL;
   float* mf = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(launch_mfcc(0, plan->dev, audio, hop, frame_size, f, mf, st));
+  VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, audio, hop, frame_size, f, mf, st));
   return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
 }
 
@@ -290,7 +321,7 @@ int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const fl
   if (!frames || !ring || !count || !labels || !mfcc_scratch) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(launch_mfcc(0, plan->dev, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
+  VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
   return (int)launch_stream_ffn(ffn->net, mfcc_scratch, ring, count, n_streams, plan->host.mfcc_n,
                                 labels, st);
 }

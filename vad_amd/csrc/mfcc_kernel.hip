@@ -23,6 +23,7 @@
 //            weights, log10, partial lifter x DCT sums.
 //   phase 3  partials of the 8 waves summed through LDS, coalesced store.
 #include "vad_common.h"
+#include "mel_tables.h"
 
 namespace vad {
 
@@ -32,7 +33,8 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kGroups = kThreads / 16;  // frames per phase-1 pass
 constexpr int kColStride = 17;   // float2 per LDS column (16 + 1 pad)
 constexpr int kGroupScratch = 16 * kColStride;  // float2 per frame group
-constexpr int kPStride = kBins + 1;             // floats per P row (bank pad)
+constexpr int kPStride = kBins + 4;  // floats per P row: 16-B aligned rows, conflict-free
+                                     // ds_read_b128 (260 = 4 mod 64 dwords)
 
 enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 
@@ -202,18 +204,71 @@ __device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
   }
 }
 
+// log10 of a positive energy: native v_log_f32 (with a pre-scale for tiny
+// inputs) times log10(2) -- ~1e-7 relative, far inside the 1e-4 budget.
+__device__ __forceinline__ float log10_pos(float e) {
+  const bool tiny = e < 0x1p-100f;
+  const float x = tiny ? e * 0x1p64f : e;
+  const float l2 = __builtin_amdgcn_logf(x);  // log2
+  return fmaf(l2, 0.30102999566398120f, tiny ? -19.26591972249479649f : 0.f);
+}
+
+// Phase 2 specialised for a compile-time filterbank T (mel_tables.h): wave W
+// owns filters [band[W], band[W+1]); every bin of the band is read once from
+// the frame's LDS row as a 16-B vector and fed to its (at most two) filters
+// with literal weights; log10; partial lifter x DCT sums.
+// Phase 2 specialised for a compile-time filterbank T (mel_tables.h): wave W
+// owns filters [band[W], band[W+1]); every bin of its band is read once from
+// the frame's LDS row as a 16-B vector and fed to its (at most two) filters,
+// then log10 and the partial lifter x DCT sums.  The bodies are generated
+// (mel_code.h) as straight-line v_fmac_f32 with 32-bit literal weights.
+template <class T, int W>
+__device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
+                                              float (&acc)[kMaxCoefs]);
+
+#include "mel_code.h"
+
+template <class T, int W>
+__device__ __forceinline__ void mel_band(const float* __restrict__ prow, int z,
+                                         float (&acc)[kMaxCoefs]) {
+  (void)z;
+  mel_band_code<T, W>(static_cast<const float*>(__builtin_assume_aligned(prow, 16)), acc);
+}
+
+template <class T>
+__device__ __forceinline__ void mel_dispatch(int wave, const float* prow, int z,
+                                             float (&acc)[kMaxCoefs]) {
+  switch (wave) {
+    case 0: mel_band<T, 0>(prow, z, acc); break;
+    case 1: mel_band<T, 1>(prow, z, acc); break;
+    case 2: mel_band<T, 2>(prow, z, acc); break;
+    case 3: mel_band<T, 3>(prow, z, acc); break;
+    case 4: mel_band<T, 4>(prow, z, acc); break;
+    case 5: mel_band<T, 5>(prow, z, acc); break;
+    case 6: mel_band<T, 6>(prow, z, acc); break;
+    default: mel_band<T, 7>(prow, z, acc); break;
+  }
+}
+
 constexpr int kPartStride = kMaxCoefs + 1;  // floats per (wave, frame) partial row
 
 // Phases 2 + 3 for one tile: mel / log / DCT partials per wave, summed
-// through LDS, coalesced store of the tile's MFCC rows.
+// through LDS, coalesced store of the tile's MFCC rows.  SPEC 0 = runtime
+// plan, 1 = Mel26, 2 = Mel40 (compile-time tables).
+template <int SPEC>
 __device__ __forceinline__ void tile_mfcc(const MfccDev* __restrict__ plan, const float* P,
                                           float* part, int tid, int wave, int lane, int64_t f0,
-                                          int64_t n_frames, int mfcc_n, float* __restrict__ out) {
+                                          int64_t n_frames, int mfcc_n_rt, float* __restrict__ out) {
+  constexpr int NC = SPEC == 1 ? Mel26::NC : SPEC == 2 ? Mel40::NC : 0;
+  const int mfcc_n = NC > 0 ? NC : mfcc_n_rt;
   __syncthreads();
   float acc[kMaxCoefs];
-  mel_log_dct(plan, P + lane * kPStride, plan->wave_fbeg[wave], plan->wave_fend[wave], acc);
+  const int z = __builtin_amdgcn_readfirstlane((int)(f0 >> 48));  // 0, opaque per tile
+  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, P + lane * kPStride, z, acc);
+  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, P + lane * kPStride, z, acc);
+  else mel_log_dct(plan, P + lane * kPStride, plan->wave_fbeg[wave], plan->wave_fend[wave], acc);
 #pragma unroll
-  for (int c = 0; c < kMaxCoefs; ++c) part[(wave * 64 + lane) * kPartStride + c] = acc[c];
+  for (int c = 0; c < (NC > 0 ? NC : kMaxCoefs); ++c) part[(wave * 64 + lane) * kPartStride + c] = acc[c];
   __syncthreads();
   const int64_t nf = (n_frames - f0) < kTile ? (n_frames - f0) : kTile;
   for (int i = tid; i < nf * mfcc_n; i += kThreads) {
@@ -226,7 +281,7 @@ __device__ __forceinline__ void tile_mfcc(const MfccDev* __restrict__ plan, cons
   __syncthreads();
 }
 
-template <int MODE, int NZ, bool VEC2, int LEN>
+template <int MODE, int NZ, bool VEC2, int LEN, int SPEC>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
@@ -255,7 +310,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // the taps carry the FFT path's 2^-20: undo it on true spectra (exact)
         P[lf * kPStride + k] = (f < n_frames) ? src[f * kBins + k] * 0x1p20f : 0.f;
       }
-      tile_mfcc(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
+      tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
     }
   } else {
     float2* gscr = scr + grp * kGroupScratch;
@@ -306,7 +361,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         }
       }
       if constexpr (MODE == kAudioToMfcc)
-        tile_mfcc(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
+        tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -329,7 +384,7 @@ static int num_cus() {
   return n;
 }
 
-template <int MODE, int NZ, bool VEC2, int LEN = 0>
+template <int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0>
 static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
@@ -338,24 +393,29 @@ static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN>), dim3(grid), dim3(kThreads), smem, st, plan,
+  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC>), dim3(grid), dim3(kThreads), smem, st, plan,
                      src, stride, len, n, out);
   return hipGetLastError();
 }
 
 template <int MODE>
-static hipError_t launch_m(const MfccDev* plan, const float* src, int64_t stride, int len,
+static hipError_t launch_m(const MfccDev* plan, int spec, const float* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int used = len < kFftN ? len : kFftN;
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) & 7) == 0) && ((stride & 1) == 0) &&
                     ((used & 1) == 0);
-  if (used == 400 && vec2)  // the reference framing (config.py:21): fully specialised
+  if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
+    if (MODE == kAudioToMfcc && spec == 1)
+      return launch_t<MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
+    if (MODE == kAudioToMfcc && spec == 2)
+      return launch_t<MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
     return launch_t<MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
+  }
   if (used <= 32 * 13) {
     return vec2 ? launch_t<MODE, 13, true>(plan, src, stride, len, n, out, st)
                 : launch_t<MODE, 13, false>(plan, src, stride, len, n, out, st);
@@ -364,13 +424,16 @@ static hipError_t launch_m(const MfccDev* plan, const float* src, int64_t stride
               : launch_t<MODE, 16, false>(plan, src, stride, len, n, out, st);
 }
 
-hipError_t launch_mfcc(int mode, const MfccDev* plan, const float* src, int64_t stride, int len,
-                       int64_t n, float* out, hipStream_t st) {
+hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
+                       int len, int64_t n, float* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (mode) {
-    case kAudioToMfcc: return launch_m<kAudioToMfcc>(plan, src, stride, len, n, out, st);
-    case kAudioToSpec: return launch_m<kAudioToSpec>(plan, src, stride, len, n, out, st);
-    default: return launch_t<kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
+    case kAudioToMfcc: return launch_m<kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
+    case kAudioToSpec: return launch_m<kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
+    default:
+      if (spec == 1) return launch_t<kSpecToMfcc, 13, false, 0, 1>(plan, src, 0, 0, n, out, st);
+      if (spec == 2) return launch_t<kSpecToMfcc, 13, false, 0, 2>(plan, src, 0, 0, n, out, st);
+      return launch_t<kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
   }
 }
 

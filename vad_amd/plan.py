@@ -63,6 +63,14 @@ class MfccPlan:
     def handle(self):
         return self._h
 
+    @property
+    def variant(self):
+        """0 = runtime tables, 1/2 = compile-time Mel26/Mel40 kernel."""
+        return int(lib().vad_mfcc_plan_variant(self._h))
+
+    def set_variant(self, v):
+        check(lib().vad_mfcc_plan_set_variant(self._h, int(v)), "vad_mfcc_plan_set_variant")
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value and _lib._lib is not None:
