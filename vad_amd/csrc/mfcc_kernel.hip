@@ -22,7 +22,10 @@
 //            by tap count at plan time): wave-uniform tap loop with scalar
 //            weights, log10, partial lifter x DCT sums.
 //   phase 3  partials of the 8 waves summed through LDS, coalesced store.
+#include <stdlib.h>
+
 #include "vad_common.h"
+#include "fft_pk.h"
 #include "mel_tables.h"
 
 namespace vad {
@@ -43,27 +46,27 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 // address clamped into the frame, so all NZ loads of a pass are in flight
 // at once; the zero padding (x[t] = 0 for t >= len) is applied later by
 // pad_stage_a, at first use.  LEN > 0 fixes the frame length at compile time
-// (400 for clips); VEC2 (8-byte aligned frames of even length) loads float2.
+// (400 for clips); VEC2 (8-byte aligned frames of even length) loads 8 B.
 template <int NZ, bool VEC2, int LEN>
 __device__ __forceinline__ void load_stage_a(const float* __restrict__ fr, int len_rt, int n2,
-                                             float2 (&u)[NZ]) {
+                                             v2f (&u)[NZ]) {
   const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
   for (int n1 = 0; n1 < NZ; ++n1) {
     const int t = 32 * n1 + 2 * n2;
     if constexpr (VEC2) {
       const int tc = t < len - 2 ? t : len - 2;
-      u[n1] = *reinterpret_cast<const float2*>(fr + tc);
+      u[n1] = *reinterpret_cast<const v2f*>(fr + tc);
     } else {
       const int t0 = t < len - 1 ? t : len - 1;
       const int t1 = t + 1 < len - 1 ? t + 1 : len - 1;
-      u[n1] = make_float2(fr[t0], fr[t1]);
+      u[n1] = (v2f){fr[t0], fr[t1]};
     }
   }
 }
 
 template <int NZ, int LEN>
-__device__ __forceinline__ void pad_stage_a(int len_rt, int n2, float2 (&u)[NZ]) {
+__device__ __forceinline__ void pad_stage_a(int len_rt, int n2, v2f (&u)[NZ]) {
   const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
   for (int n1 = 0; n1 < NZ; ++n1) {
@@ -83,8 +86,8 @@ __device__ __forceinline__ void pad_stage_a(int len_rt, int n2, float2 (&u)[NZ])
 //   registers into (Z[16 m], Z[256 - 16 m]) pairs; its m = 0 pair holds the
 //   two self-partnered bins 0 and 128, fixed up explicitly.
 struct LaneConsts {
-  float2 twa[16];  // W256^(j k1)
-  float2 twb[8];   // W512^kE(m)
+  v2f twa[16];     // W256^(j k1)
+  v2f twb[8];      // W512^kE(m)
   int cE, cO;
   int e0, es;      // kE(m) = e0 + es*m
   int o0;          // kO(m) = o0 - es*m (m >= 1)
@@ -105,66 +108,68 @@ __device__ __forceinline__ void lane_consts(const MfccDev* __restrict__ plan, in
   L.es = L.col0 ? 16 : 32;
   L.o0 = 256 - L.cE;
   L.kO0 = L.col0 ? 128 : 256 - L.cE;
+  const v2f* ta = reinterpret_cast<const v2f*>(plan->tw_a);
+  const v2f* tb = reinterpret_cast<const v2f*>(plan->tw_b);
 #pragma unroll
-  for (int k1 = 0; k1 < 16; ++k1) L.twa[k1] = plan->tw_a[j * 16 + k1];
+  for (int k1 = 0; k1 < 16; ++k1) L.twa[k1] = ta[j * 16 + k1];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) L.twb[m] = plan->tw_b[L.e0 + L.es * m];
+  for (int m = 0; m < 8; ++m) L.twb[m] = tb[L.e0 + L.es * m];
 }
 
 // Phase 1 for one frame of a 16-lane group: power spectrum into prow
 // (LDS row, or a global row in spectrum mode).  SCALE multiplies |2X|^2 into
 // P = |X/512|^2 (2^-20); the MFCC modes fold that factor into the mel taps.
+// Every complex operation is packed fp32 (fft_pk.h).
 template <int NZ, int LEN, bool SCALE>
-__device__ __forceinline__ void frame_power(float2 (&u_in)[NZ], int len, const LaneConsts& L, int j,
-                                            float2* __restrict__ scr, float* __restrict__ prow) {
+__device__ __forceinline__ void frame_power(v2f (&u_in)[NZ], int len, const LaneConsts& L, int j,
+                                            v2f* __restrict__ scr, float* __restrict__ prow) {
   // ---- stage A: DFT16 over n1 for n2 = j, twiddle W256^(j k1), to LDS ----
   pad_stage_a<NZ, LEN>(len, j, u_in);
-  float2 u[16];
+  v2f u[16];
 #pragma unroll
   for (int n = 0; n < NZ; ++n) u[n] = u_in[n];
-  dft16<NZ>(u);
+  pk::dft16<NZ>(u);
 #pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) u[k1] = cmul(u[k1], L.twa[k1]);
+  for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) scr[k1 * kColStride + j] = u[k1];
   __builtin_amdgcn_wave_barrier();
 
   // ---- stage B: even half of column cE, odd half of column cO ----------
-  float2 E[8], O[8];
+  v2f E[8], O[8];
   {
-    float2 col[16];
+    v2f col[16];
 #pragma unroll
     for (int n = 0; n < 16; ++n) col[n] = scr[L.cE * kColStride + n];
-    dft16_even(col, E);  // E[m] = Z[cE + 32 m]
+    pk::dft16_even(col, E);  // E[m] = Z[cE + 32 m]
 #pragma unroll
     for (int n = 0; n < 16; ++n) col[n] = scr[L.cO * kColStride + n];
-    dft16_odd(col, O);   // O[m] = Z[cO + 32 m + 16]
+    pk::dft16_odd(col, O);   // O[m] = Z[cO + 32 m + 16]
   }
   __builtin_amdgcn_wave_barrier();
 
   // ---- real-FFT split on pairs (a, b) = (Z[k], Z[256-k]):
   //   2 X[k] = S - i W^k D,  2 X[256-k] = conj(S) - i conj(W^k D),
   //   S = a + conj(b), D = a - conj(b),  W = W512
+  //   U = (Re 2X[k], Re 2X[256-k]), V = (Im 2X[k], Im 2X[256-k])
   // column-0 lane: E' = (Z0, Z16, ..., Z112), O'[7-m] = Z[256 - 16 m]
-  const float2 Ep[8] = {E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3]};
-  const float2 Op[8] = {O[4], E[5], O[5], E[6], O[6], E[7], O[7], E[4]};
-  constexpr float sc = SCALE ? 0x1p-20f : 1.0f;
+  const v2f Ep[8] = {E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3]};
+  const v2f Op[8] = {O[4], E[5], O[5], E[6], O[6], E[7], O[7], E[4]};
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    const float2 a = make_float2(L.col0 ? Ep[m].x : E[m].x, L.col0 ? Ep[m].y : E[m].y);
-    const float2 b = make_float2(L.col0 ? Op[7 - m].x : O[7 - m].x,
-                                 L.col0 ? Op[7 - m].y : O[7 - m].y);
-    const float2 S = make_float2(a.x + b.x, a.y - b.y);
-    const float2 D = make_float2(a.x - b.x, a.y + b.y);
-    const float2 T = cmul(D, L.twb[m]);
-    const float xr = S.x + T.y, xi = S.y - T.x;        // 2 X[k]
-    const float yr = S.x - T.y, yi = -S.y - T.x;       // 2 X[256-k]
-    float pk = fmaf(xr, xr, xi * xi) * sc;
-    float pn = fmaf(yr, yr, yi * yi) * sc;
+    const v2f a = L.col0 ? Ep[m] : E[m];
+    const v2f b = L.col0 ? Op[7 - m] : O[7 - m];
+    const v2f S = pk::add_conj(a, b);
+    const v2f T = pk::cmul(pk::sub_conj(a, b), L.twb[m]);
+    const v2f U = pk::split_u(S, T);
+    const v2f V = pk::split_v(S, T);
+    v2f p2 = U * U + V * V;  // (|2X[k]|^2, |2X[256-k]|^2)
+    if constexpr (SCALE) p2 = p2 * 0x1p-20f;
+    float pk = p2.x, pn = p2.y;
     if (m == 0) {  // lane 14: bins 0 and 128 are their own partners
-      const float s0 = a.x + a.y;                       // X[0] = Re Z0 + Im Z0
-      const float p0 = 4.f * s0 * s0 * sc;
-      const float p128 = 4.f * fmaf(b.x, b.x, b.y * b.y) * sc;  // X[128] = conj(Z128)
+      const float s0 = a.x + a.y;                                 // X[0] = Re Z0 + Im Z0
+      const float p0 = 4.f * s0 * s0 * (SCALE ? 0x1p-20f : 1.f);
+      const float p128 = 4.f * fmaf(b.x, b.x, b.y * b.y) * (SCALE ? 0x1p-20f : 1.f);
       pk = L.col0 ? p0 : pk;
       pn = L.col0 ? p128 : pn;
     }
@@ -281,13 +286,16 @@ __device__ __forceinline__ void tile_mfcc(const MfccDev* __restrict__ plan, cons
   __syncthreads();
 }
 
-template <int MODE, int NZ, bool VEC2, int LEN, int SPEC>
+// DIAG (diagnostic builds only, VAD_DIAG env): 1 = skip the FFT (phase 1
+// keeps its loads and P stores), 2 = skip phases 2-3, 3 = both (loads only),
+// 4 = FFT on register data without loads, no phases 2-3.  Outputs are wrong.
+template <int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* P = reinterpret_cast<float*>(smem);                                   // [64][257]
-  float2* scr = reinterpret_cast<float2*>(smem + kTile * kPStride * sizeof(float));
+  v2f* scr = reinterpret_cast<v2f*>(smem + kTile * kPStride * sizeof(float));
   float* part = reinterpret_cast<float*>(scr);            // phase 3 reuse: [wave][64][17]
 
   const int tid = threadIdx.x;
@@ -313,12 +321,12 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
     }
   } else {
-    float2* gscr = scr + grp * kGroupScratch;
+    v2f* gscr = scr + grp * kGroupScratch;
     LaneConsts L;
     lane_consts(plan, j, L);
     // software pipeline: the samples of the next pass are in flight while
     // the current pass computes
-    float2 bufA[NZ], bufB[NZ];
+    v2f bufA[NZ], bufB[NZ];
     const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
     int64_t tile = blockIdx.x;
     {
@@ -331,7 +339,12 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       {  // prefetch pass 1 of this tile
         int64_t f = f0 + kGroups + grp;
         f = f < flast ? f : flast;
-        load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufB);
+        if constexpr (DIAG == 4) {
+#pragma unroll
+          for (int n = 0; n < NZ; ++n) bufB[n] = (v2f){(float)(f + n), (float)(j - n)};
+        } else {
+          load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufB);
+        }
       }
       // keep the scheduler from hoisting the next pass's FFT above this
       // pass (that would wait on the loads just issued and defeat the
@@ -342,14 +355,23 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         if constexpr (MODE == kAudioToSpec) {
           if (f < n_frames) frame_power<NZ, LEN, true>(bufA, len, L, j, gscr, out + f * kBins);
         } else {
-          frame_power<NZ, LEN, false>(bufA, len, L, j, gscr, P + grp * kPStride);
+          if constexpr (DIAG == 1 || DIAG == 3) {
+            P[grp * kPStride + j] = bufA[j % NZ].x + bufA[(j + 5) % NZ].y;
+          } else {
+            frame_power<NZ, LEN, false>(bufA, len, L, j, gscr, P + grp * kPStride);
+          }
         }
       }
       __builtin_amdgcn_sched_barrier(0);
       {  // prefetch pass 0 of the next tile
         int64_t f = (tile + gridDim.x) * kTile + grp;
         f = f < flast ? f : flast;
-        load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
+        if constexpr (DIAG == 4) {
+#pragma unroll
+          for (int n = 0; n < NZ; ++n) bufA[n] = (v2f){(float)(f - n), (float)(j + n)};
+        } else {
+          load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       {  // pass 1
@@ -357,18 +379,27 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         if constexpr (MODE == kAudioToSpec) {
           if (f < n_frames) frame_power<NZ, LEN, true>(bufB, len, L, j, gscr, out + f * kBins);
         } else {
-          frame_power<NZ, LEN, false>(bufB, len, L, j, gscr, P + (kGroups + grp) * kPStride);
+          if constexpr (DIAG == 1 || DIAG == 3) {
+            P[(kGroups + grp) * kPStride + j] = bufB[j % NZ].x + bufB[(j + 5) % NZ].y;
+          } else {
+            frame_power<NZ, LEN, false>(bufB, len, L, j, gscr, P + (kGroups + grp) * kPStride);
+          }
         }
       }
-      if constexpr (MODE == kAudioToMfcc)
+      if constexpr (MODE == kAudioToMfcc && DIAG <= 1)
         tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
+      if constexpr (DIAG >= 2) {
+        __syncthreads();
+        if (tid < 64) out[f0 * 13 + tid] = P[tid * kPStride + (tid & 15)];
+        __syncthreads();
+      }
     }
   }
 }
 
 size_t mfcc_smem_bytes() {
   const size_t p = kTile * kPStride * sizeof(float);  // 65792 B, 16-B multiple
-  const size_t s = kGroups * kGroupScratch * sizeof(float2);
+  const size_t s = kGroups * kGroupScratch * sizeof(v2f);
   const size_t part = kWaves * 64 * kPartStride * sizeof(float);
   return p + (s > part ? s : part);
 }
@@ -384,7 +415,7 @@ static int num_cus() {
   return n;
 }
 
-template <int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0>
+template <int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0>
 static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
@@ -393,12 +424,12 @@ static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC, DIAG>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC>), dim3(grid), dim3(kThreads), smem, st, plan,
+  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC, DIAG>), dim3(grid), dim3(kThreads), smem, st, plan,
                      src, stride, len, n, out);
   return hipGetLastError();
 }
@@ -410,8 +441,14 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const float* src, int6
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) & 7) == 0) && ((stride & 1) == 0) &&
                     ((used & 1) == 0);
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
-    if (MODE == kAudioToMfcc && spec == 1)
+    if (MODE == kAudioToMfcc && spec == 1) {
+      static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
+      if (diag == 1) return launch_t<MODE, 13, true, 400, 1, 1>(plan, src, stride, len, n, out, st);
+      if (diag == 2) return launch_t<MODE, 13, true, 400, 1, 2>(plan, src, stride, len, n, out, st);
+      if (diag == 3) return launch_t<MODE, 13, true, 400, 1, 3>(plan, src, stride, len, n, out, st);
+      if (diag == 4) return launch_t<MODE, 13, true, 400, 1, 4>(plan, src, stride, len, n, out, st);
       return launch_t<MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
+    }
     if (MODE == kAudioToMfcc && spec == 2)
       return launch_t<MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
     return launch_t<MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
