@@ -14,6 +14,7 @@
 namespace vad {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 
 constexpr float kC8 = 0.70710678118654752440f;   // cos(pi/4)
 constexpr float kC16 = 0.92387953251128675613f;  // cos(pi/8)

@@ -130,7 +130,8 @@ def emit_code(name, info):
         k1 = los[fe - 1] + lens[fe - 1]
         nq = (k1 - k0 + 3) // 4
         for q in range(nq):
-            out.append(f"  const float4 q{q} = *reinterpret_cast<const float4*>(prow + {k0 + 4 * q});")
+            out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
+                       f"__builtin_assume_aligned(prow + {k0 + 4 * q}, 16));")
         comp = "xyzw"
         first = {}
         for m in range(fb, fe):
