@@ -66,23 +66,40 @@ __device__ __forceinline__ int argmax_classes(const f32x4 z, int n_classes) {
 }
 
 // One MFMA layer: out[mt] = bias + sum over (t, r) of A[mt][t*4+r] x in[t][r].
+// The K loop is outermost so the TO independent accumulator chains interleave
+// (v_mfma_f32_16x16x4_f32: 32-cycle issue, 40-cycle dependent latency).
 template <int TO, int TI>
 __device__ __forceinline__ void dense_layer(const float* __restrict__ a, const float* __restrict__ b,
                                             const f32x4 (&in)[TI], f32x4 (&out)[TO], bool relu) {
+  // TO == 1: two chains (even / odd K-steps) so consecutive MFMAs never wait
+  // on each other; summed at the end (fixed order: deterministic).
+  constexpr int NCH = TO == 1 ? 2 : 1;
+  f32x4 acc[TO][NCH];
 #pragma unroll
   for (int mt = 0; mt < TO; ++mt) {
-    f32x4 acc = {b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
+    acc[mt][0] = (f32x4){b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
+    if constexpr (NCH == 2) acc[mt][NCH - 1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
-    for (int t = 0; t < TI; ++t) {
+  for (int t = 0; t < TI; ++t) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(mt * TI + t) * 4 + r], in[t][r], acc, 0, 0, 0);
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int mt = 0; mt < TO; ++mt) {
+        f32x4& ac = acc[mt][(t * 4 + r) % NCH];
+        ac = __builtin_amdgcn_mfma_f32_16x16x4f32(a[(mt * TI + t) * 4 + r], in[t][r], ac, 0, 0, 0);
+      }
     }
+  }
+#pragma unroll
+  for (int mt = 0; mt < TO; ++mt) {
+    f32x4 v = acc[mt][0];
+    if constexpr (NCH == 2) v = v + acc[mt][1];
     if (relu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = relu_nan(acc[r]);
+      for (int r = 0; r < 4; ++r) v[r] = relu_nan(v[r]);
     }
-    out[mt] = acc;
+    out[mt] = v;
   }
 }
 
@@ -105,16 +122,19 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
   using TP = Topo<KS0, T1, T2, T3, T4>;
   f32x4 h1[T1];
 #pragma unroll
-  for (int mt = 0; mt < T1; ++mt) {
-    f32x4 acc = {fb[mt * 4 + 0], fb[mt * 4 + 1], fb[mt * 4 + 2], fb[mt * 4 + 3]};
+  for (int mt = 0; mt < T1; ++mt) h1[mt] = (f32x4){fb[mt * 4 + 0], fb[mt * 4 + 1], fb[mt * 4 + 2], fb[mt * 4 + 3]};
 #pragma unroll
-    for (int s = 0; s < KS0; ++s)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[mt * KS0 + s], x[s], acc, 0, 0, 0);
-    if (TP::NL > 1) {
+  for (int s = 0; s < KS0; ++s) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = relu_nan(acc[r]);
+    for (int mt = 0; mt < T1; ++mt)
+      h1[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[mt * KS0 + s], x[s], h1[mt], 0, 0, 0);
+  }
+  if (TP::NL > 1) {
+#pragma unroll
+    for (int mt = 0; mt < T1; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h1[mt][r] = relu_nan(h1[mt][r]);
     }
-    h1[mt] = acc;
   }
   if constexpr (TP::NL == 1) return h1[0];
   else {
@@ -179,6 +199,104 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
     }
     const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
     if (g == 0 && valid) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+  }
+}
+
+// Windows of an MFCC sequence, 64 per block iteration (4 waves x 16):
+//   A  the 68 MFCC rows the chunk needs are staged in LDS (coalesced);
+//   B  every (window, coefficient) feature triple is computed once, by one
+//      thread, from LDS (fp64 window statistics), into an LDS feature tile;
+//   C  each wave runs the MFMA chain on 16 windows with its layer-0 B
+//      operands read from the tile, then the argmax.
+constexpr int kChunk = 64;
+constexpr int kXStride = 65;  // floats per feature row (64 + 1: bank spread)
+
+template <int KS0, int T1, int T2, int T3, int T4, int MN>
+__global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float* __restrict__ mfcc,
+                                                         int64_t n_rows, int mfcc_n_rt, int mode,
+                                                         uint8_t* __restrict__ labels) {
+  using TP = Topo<KS0, T1, T2, T3, T4>;
+  __shared__ float rows[(kChunk + 4) * kMaxCoefs];
+  __shared__ float X[kChunk * kXStride];
+  const int mfcc_n = MN > 0 ? MN : mfcc_n_rt;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wv = tid >> 6;
+  const int g = lane >> 4;
+  const int jw = lane & 15;
+  const int in_dim = net.dims[0];
+  const int nfeat = 3 * mfcc_n;
+
+  float fa[TP::NA];
+  float fb[TP::NB];
+#pragma unroll
+  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
+#pragma unroll
+  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+
+  const int64_t n_frames = n_rows + 5;
+  const int64_t n_chunks = (n_rows + kChunk - 1) / kChunk;
+  // rows of a chunk: (kChunk + 4) x mfcc_n floats, <= 4 per thread; the next
+  // chunk's are loaded into registers while the current one computes
+  constexpr int kRowRegs = ((kChunk + 4) * kMaxCoefs + 255) / 256;
+  float pre[kRowRegs];
+  auto load_rows = [&](int64_t ch) {
+    const int64_t base = ch * kChunk;
+    const int64_t avail = ch < n_chunks ? n_frames - base : 0;
+    const int nr = (int)(avail < kChunk + 4 ? avail : kChunk + 4);
+#pragma unroll
+    for (int q = 0; q < kRowRegs; ++q) {
+      const int i = tid + 256 * q;
+      pre[q] = i < nr * mfcc_n ? mfcc[base * mfcc_n + i] : 0.f;
+    }
+  };
+  load_rows(blockIdx.x);
+  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+    const int64_t base = ch * kChunk;
+    // ---- A: rows base .. base+67 (prefetched) ------------------------------
+#pragma unroll
+    for (int q = 0; q < kRowRegs; ++q) {
+      const int i = tid + 256 * q;
+      if (i < (kChunk + 4) * mfcc_n) {
+        const int r = i / mfcc_n, c = i - r * mfcc_n;
+        rows[r * kMaxCoefs + c] = pre[q];
+      }
+    }
+    __syncthreads();
+    load_rows(ch + gridDim.x);
+    // ---- B: features (sklearn_analyser.py:52-69 / file_processing.py:51-66)
+    const int64_t nwin64 = n_rows - base;
+    const int nwin = (int)(nwin64 < kChunk ? nwin64 : kChunk);
+    for (int i = tid; i < nwin * mfcc_n; i += 256) {
+      const int w = i / mfcc_n, c = i - w * mfcc_n;
+      const float* rw = rows + w * kMaxCoefs + c;
+      const double a0 = rw[0], a1 = rw[kMaxCoefs], a2 = rw[2 * kMaxCoefs], a3 = rw[3 * kMaxCoefs],
+                   a4 = rw[4 * kMaxCoefs];
+      double mn = a2;
+      if (mode == VAD_FEAT_ANALYSER) {
+        const double mean = ((((a0 + a1) + a2) + a3) + a4) / 5.0;
+        const double d0 = a0 - mean, d1 = a1 - mean, d2 = a2 - mean, d3 = a3 - mean, d4 = a4 - mean;
+        const double var = ((((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3) + d4 * d4) / 5.0;
+        mn = d2 / sqrt(var);
+      }
+      float* xw = X + w * kXStride;
+      xw[c] = (float)mn;
+      xw[mfcc_n + c] = (float)(a3 - a1);
+      xw[2 * mfcc_n + c] = (float)((a4 - mn) - (mn - a0));
+    }
+    __syncthreads();
+    // ---- C: MFMA chain, 16 windows per wave --------------------------------
+    const int wl = wv * 16 + jw;
+    const int64_t w = base + wl;
+    float x[KS0];
+#pragma unroll
+    for (int s = 0; s < KS0; ++s) {
+      const int f = 4 * s + g;
+      x[s] = (f < in_dim && f < nfeat && wl < nwin) ? X[wl * kXStride + f] : 0.f;
+    }
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    if (g == 0 && wl < nwin) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+    __syncthreads();
   }
 }
 
@@ -270,10 +388,17 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
   const int64_t n_tiles = (n_rows + 15) / 16;
   int64_t blocks = (n_tiles + 3) / 4;
   if (blocks > 2048) blocks = 2048;
-  if (src == kFromMfcc)
-    hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, kFromMfcc>), dim3((int)blocks), dim3(256), 0,
-                       st, net, in, n_rows, mfcc_n, mode, labels);
-  else
+  if (src == kFromMfcc) {
+    int64_t chunks = (n_rows + kChunk - 1) / kChunk;
+    const int64_t cap = 8 * 256;  // persistent-ish: fragments load once per block
+    if (chunks > cap) chunks = cap;
+    if (mfcc_n == 13)
+      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, 13>), dim3((int)chunks), dim3(256), 0,
+                         st, net, in, n_rows, mfcc_n, mode, labels);
+    else
+      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, 0>), dim3((int)chunks), dim3(256), 0,
+                         st, net, in, n_rows, mfcc_n, mode, labels);
+  } else
     hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, kFromRows>), dim3((int)blocks), dim3(256), 0,
                        st, net, in, n_rows, mfcc_n, mode, labels);
   return hipGetLastError();
