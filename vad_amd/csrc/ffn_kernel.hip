@@ -19,10 +19,31 @@
 
 namespace vad {
 
-// Feature f of the window whose 5 MFCC rows are r[0..4] (row centre-2+d).
-// Analyser mode normalises the centre by the window mean/std in fp64: the
-// MFCCs are fp32, so the 5-term sums are exact and a constant window gives
-// exactly std = 0 -> 0/0 = NaN, as numpy does on the reference's fp64 rows.
+// Feature triple of coefficient c over a 5-frame window a0..a4 (frames
+// centre-2 .. centre+2): (Mn, M+1 - M-1, (M+2 - Mn) - (Mn - M-2)) with Mn the
+// centre normalised by the window mean / std (ddof 0) in analyser mode
+// (sklearn_analyser.py:52-69,103-107) or the raw centre in offline mode
+// (file_processing.py:51-66).  fp32 arithmetic; the reference's fp64 std is 0
+// exactly when all five values are equal (0/0 = NaN there), so that case is
+// tested explicitly instead of relying on fp32 rounding of the mean.
+struct Feat3 {
+  float mn, d1, d2;
+};
+
+__device__ __forceinline__ Feat3 feature_triple(float a0, float a1, float a2, float a3, float a4,
+                                                int mode) {
+  float mn = a2;
+  if (mode == VAD_FEAT_ANALYSER) {
+    const float mean = ((((a0 + a1) + a2) + a3) + a4) * 0.2f;
+    const float e0 = a0 - mean, e1 = a1 - mean, e2 = a2 - mean, e3 = a3 - mean, e4 = a4 - mean;
+    const float var = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * 0.2f;
+    const bool flat = (a0 == a1) & (a1 == a2) & (a2 == a3) & (a3 == a4);
+    mn = flat ? __builtin_nanf("") : e2 * rsqrtf(var);
+  }
+  return {mn, a3 - a1, (a4 - mn) - (mn - a0)};
+}
+
+// Feature f (0 .. 3*mfcc_n-1) of the window whose 5 MFCC rows are r0..r4.
 __device__ __forceinline__ float window_feature(const float* __restrict__ r0,
                                                const float* __restrict__ r1,
                                                const float* __restrict__ r2,
@@ -31,17 +52,8 @@ __device__ __forceinline__ float window_feature(const float* __restrict__ r0,
                                                int mode) {
   const int t = f / mfcc_n;
   const int c = f - t * mfcc_n;
-  const double a0 = r0[c], a1 = r1[c], a2 = r2[c], a3 = r3[c], a4 = r4[c];
-  if (t == 1) return (float)(a3 - a1);                        // :64 M+1 - M-1
-  double mn = a2;
-  if (mode == VAD_FEAT_ANALYSER) {                            // :103-107
-    const double mean = ((((a0 + a1) + a2) + a3) + a4) / 5.0;
-    const double d0 = a0 - mean, d1 = a1 - mean, d2 = a2 - mean, d3 = a3 - mean, d4 = a4 - mean;
-    const double var = ((((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3) + d4 * d4) / 5.0;
-    mn = d2 / sqrt(var);
-  }
-  if (t == 0) return (float)mn;
-  return (float)((a4 - mn) - (mn - a0));                      // :57-65 second deltas
+  const Feat3 ft = feature_triple(r0[c], r1[c], r2[c], r3[c], r4[c], mode);
+  return t == 0 ? ft.mn : t == 1 ? ft.d1 : ft.d2;
 }
 
 // argmax of softmax(z) with np.argmax semantics on the fp32 logits: any NaN
@@ -270,19 +282,12 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
     for (int i = tid; i < nwin * mfcc_n; i += 256) {
       const int w = i / mfcc_n, c = i - w * mfcc_n;
       const float* rw = rows + w * kMaxCoefs + c;
-      const double a0 = rw[0], a1 = rw[kMaxCoefs], a2 = rw[2 * kMaxCoefs], a3 = rw[3 * kMaxCoefs],
-                   a4 = rw[4 * kMaxCoefs];
-      double mn = a2;
-      if (mode == VAD_FEAT_ANALYSER) {
-        const double mean = ((((a0 + a1) + a2) + a3) + a4) / 5.0;
-        const double d0 = a0 - mean, d1 = a1 - mean, d2 = a2 - mean, d3 = a3 - mean, d4 = a4 - mean;
-        const double var = ((((d0 * d0 + d1 * d1) + d2 * d2) + d3 * d3) + d4 * d4) / 5.0;
-        mn = d2 / sqrt(var);
-      }
+      const Feat3 ft = feature_triple(rw[0], rw[kMaxCoefs], rw[2 * kMaxCoefs], rw[3 * kMaxCoefs],
+                                      rw[4 * kMaxCoefs], mode);
       float* xw = X + w * kXStride;
-      xw[c] = (float)mn;
-      xw[mfcc_n + c] = (float)(a3 - a1);
-      xw[2 * mfcc_n + c] = (float)((a4 - mn) - (mn - a0));
+      xw[c] = ft.mn;
+      xw[mfcc_n + c] = ft.d1;
+      xw[2 * mfcc_n + c] = ft.d2;
     }
     __syncthreads();
     // ---- C: MFMA chain, 16 windows per wave --------------------------------
