@@ -103,6 +103,10 @@ __device__ __forceinline__ void dense_layer(const float* __restrict__ a, const f
       }
     }
   }
+  // keep the whole layer's MFMAs back to back; the epilogue (bias already in,
+  // ReLU) then waits once for the last accumulator instead of interleaving
+  // accumulator reads into the next layer's MFMA stream
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int mt = 0; mt < TO; ++mt) {
     f32x4 v = acc[mt][0];
@@ -113,6 +117,7 @@ __device__ __forceinline__ void dense_layer(const float* __restrict__ a, const f
     }
     out[mt] = v;
   }
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // Network shape: KS0 layer-0 K-steps (4 features each), Tl = 16-row output
@@ -141,6 +146,7 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
     for (int mt = 0; mt < T1; ++mt)
       h1[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[mt * KS0 + s], x[s], h1[mt], 0, 0, 0);
   }
+  __builtin_amdgcn_sched_barrier(0);
   if (TP::NL > 1) {
 #pragma unroll
     for (int mt = 0; mt < T1; ++mt) {
@@ -148,6 +154,7 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
       for (int r = 0; r < 4; ++r) h1[mt][r] = relu_nan(h1[mt][r]);
     }
   }
+  __builtin_amdgcn_sched_barrier(0);
   if constexpr (TP::NL == 1) return h1[0];
   else {
     f32x4 h2[T2];
@@ -387,6 +394,17 @@ static hipError_t launch_stream_topo(const FfnDev& net, const float* newrow, flo
   return hipGetLastError();
 }
 
+static int ffn_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 template <int KS0, int T1, int T2, int T3, int T4>
 static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64_t n_rows,
                               int mfcc_n, int mode, uint8_t* labels, hipStream_t st) {
@@ -395,7 +413,9 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
   if (blocks > 2048) blocks = 2048;
   if (src == kFromMfcc) {
     int64_t chunks = (n_rows + kChunk - 1) / kChunk;
-    const int64_t cap = 8 * 256;  // persistent-ish: fragments load once per block
+    // persistent: one resident wave of blocks (2 per CU at ~200 registers),
+    // so each block loads its weight fragments once and streams its chunks
+    const int64_t cap = 2 * ffn_num_cus();
     if (chunks > cap) chunks = cap;
     if (mfcc_n == 13)
       hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, 13>), dim3((int)chunks), dim3(256), 0,
