@@ -85,7 +85,7 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     // x 2^-20: the FFT path produces |2X|^2 and P = |X/512|^2 = |2X|^2 2^-20 (exact)
     for (int t = 0; t < n; ++t) h.taps[off + t] = (float)row[lo + t] * 0x1p-20f;
     off += n;
-    cost[m] = n + 2 * mfcc_n + 8;  // taps + DCT FMAs + log, in VALU-op units
+    cost[m] = n + 8;  // taps + (==0 -> eps) + log10, in VALU-op units
   }
   // balance contiguous filter bands over the 8 waves of phase 2
   {

@@ -17,11 +17,14 @@
 //                       holds is in its own registers (column 0 is the one
 //                       exception, handled by a per-lane select);
 //              post     X[k] = (S - i W512^k D) / 2, P[k] = |X[k] / 512|^2,
-//                       written to an LDS power tile P[64][257].
-//   phase 2  one frame per lane, each wave owns a band of filters (balanced
-//            by tap count at plan time): wave-uniform tap loop with scalar
-//            weights, log10, partial lifter x DCT sums.
-//   phase 3  partials of the 8 waves summed through LDS, coalesced store.
+//                       written to an LDS power tile P[64][260].
+//   phase 2a one frame per lane, each wave owns a band of filters (balanced
+//            by tap count): mel energies, (==0 -> eps), log10 -> LDS log-mel
+//            rows.
+//   phase 2b one frame per lane, waves 0..3 own coefficients c = w + 4 i:
+//            lifter x DCT of the log-mel rows, stored to the MFCC rows.  It
+//            runs deferred, in the next tile after phase 1, on the waves that
+//            finish their FFT first -- two barriers per tile.
 #include <stdlib.h>
 
 #include "vad_common.h"
@@ -32,9 +35,9 @@ namespace vad {
 
 constexpr int kTile = 64;        // frames per workgroup tile
 constexpr int kThreads = 512;    // 8 waves
-constexpr int kWaves = kThreads / 64;
 constexpr int kGroups = kThreads / 16;  // frames per phase-1 pass
-constexpr int kColStride = 17;   // float2 per LDS column (16 + 1 pad)
+constexpr int kColStride = 18;   // complex per LDS column: 16-B aligned columns whose
+                                 // ds_read_b128 lane groups hit disjoint banks
 constexpr int kGroupScratch = 16 * kColStride;  // float2 per frame group
 constexpr int kPStride = kBins + 4;  // floats per P row: 16-B aligned rows, conflict-free
                                      // ds_read_b128 (260 = 4 mod 64 dwords)
@@ -116,37 +119,56 @@ __device__ __forceinline__ void lane_consts(const MfccDev* __restrict__ plan, in
   for (int m = 0; m < 8; ++m) L.twb[m] = tb[L.e0 + L.es * m];
 }
 
-// Phase 1 for one frame of a 16-lane group: power spectrum into prow
-// (LDS row, or a global row in spectrum mode).  SCALE multiplies |2X|^2 into
-// P = |X/512|^2 (2^-20); the MFCC modes fold that factor into the mel taps.
-// Every complex operation is packed fp32 (fft_pk.h).
-template <int NZ, int LEN, bool SCALE>
-__device__ __forceinline__ void frame_power(v2f (&u_in)[NZ], int len, const LaneConsts& L, int j,
-                                            v2f* __restrict__ scr, float* __restrict__ prow) {
-  // ---- stage A: DFT16 over n1 for n2 = j, twiddle W256^(j k1), to LDS ----
+// Phase 1 for one frame of a 16-lane group, in three steps so that a wave
+// can overlap one pass's LDS transpose with the next pass's stage A:
+//   stage_a   DFT16 over n1 for n2 = j, twiddle W256^(j k1) (registers)
+//   store_a   the 16 results to the group's LDS transpose block
+//   read_b    column cE and column cO back (16 ds_read_b128, left in flight)
+//   finish_b  even half of column cE, odd half of column cO, real-FFT split,
+//             power into prow (LDS row, or a global row in spectrum mode).
+// SCALE multiplies |2X|^2 into P = |X/512|^2 (2^-20); the MFCC modes fold
+// that factor into the mel taps.  Every complex operation is packed fp32
+// (fft_pk.h).
+template <int NZ, int LEN>
+__device__ __forceinline__ void stage_a(v2f (&u_in)[NZ], int len, const LaneConsts& L, int j,
+                                        v2f (&u)[16]) {
   pad_stage_a<NZ, LEN>(len, j, u_in);
-  v2f u[16];
 #pragma unroll
   for (int n = 0; n < NZ; ++n) u[n] = u_in[n];
   pk::dft16<NZ>(u);
 #pragma unroll
   for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
+}
+
+__device__ __forceinline__ void store_a(const v2f (&u)[16], v2f* __restrict__ scr, int j) {
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) scr[k1 * kColStride + j] = u[k1];
-  __builtin_amdgcn_wave_barrier();
+}
 
-  // ---- stage B: even half of column cE, odd half of column cO ----------
-  v2f E[8], O[8];
-  {
-    v2f col[16];
+__device__ __forceinline__ void read_b(const LaneConsts& L, const v2f* __restrict__ scr,
+                                       v2f (&col)[32]) {
+  const v4f* ce = reinterpret_cast<const v4f*>(__builtin_assume_aligned(scr + L.cE * kColStride, 16));
+  const v4f* co = reinterpret_cast<const v4f*>(__builtin_assume_aligned(scr + L.cO * kColStride, 16));
 #pragma unroll
-    for (int n = 0; n < 16; ++n) col[n] = scr[L.cE * kColStride + n];
-    pk::dft16_even(col, E);  // E[m] = Z[cE + 32 m]
-#pragma unroll
-    for (int n = 0; n < 16; ++n) col[n] = scr[L.cO * kColStride + n];
-    pk::dft16_odd(col, O);   // O[m] = Z[cO + 32 m + 16]
+  for (int q = 0; q < 8; ++q) {
+    const v4f t = ce[q];
+    col[2 * q] = t.xy;
+    col[2 * q + 1] = t.zw;
   }
-  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const v4f t = co[q];
+    col[16 + 2 * q] = t.xy;
+    col[16 + 2 * q + 1] = t.zw;
+  }
+}
+
+template <bool SCALE>
+__device__ __forceinline__ void finish_b(const LaneConsts& L, v2f (&col)[32],
+                                         float* __restrict__ prow) {
+  v2f E[8], O[8];
+  pk::dft16_even(*reinterpret_cast<v2f(*)[16]>(&col[0]), E);   // E[m] = Z[cE + 32 m]
+  pk::dft16_odd(*reinterpret_cast<v2f(*)[16]>(&col[16]), O);   // O[m] = Z[cO + 32 m + 16]
 
   // ---- real-FFT split on pairs (a, b) = (Z[k], Z[256-k]):
   //   2 X[k] = S - i W^k D,  2 X[256-k] = conj(S) - i conj(W^k D),
@@ -180,14 +202,27 @@ __device__ __forceinline__ void frame_power(v2f (&u_in)[NZ], int len, const Lane
   }
 }
 
-// Phase 2: frame `lane` of the tile, filters [fb, fe): partial lifter x DCT
-// sums in acc[].
-__device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
-                                            const float* __restrict__ prow, int fb, int fe,
-                                            float (&acc)[kMaxCoefs]) {
+// log10 of a positive energy: native v_log_f32 (with a pre-scale for tiny
+// inputs) times log10(2) -- ~1e-7 relative, far inside the 1e-4 budget.
+__device__ __forceinline__ float log10_pos(float e) {
+  const bool tiny = e < 0x1p-100f;
+  const float x = tiny ? e * 0x1p64f : e;
+  const float l2 = __builtin_amdgcn_logf(x);  // log2
+  return fmaf(l2, 0.30102999566398120f, tiny ? -19.26591972249479649f : 0.f);
+}
+
+// Log-mel rows of a tile, [64][LMS] fp32: LMS is 4 x odd, so the
+// frame-per-lane ds_read_b128 of phase 2b hits disjoint banks.
+template <int SPEC>
+constexpr int lm_stride() { return SPEC == 1 ? 28 : SPEC == 2 ? 44 : kMaxFilters + 4; }
+constexpr int kLmFloats = kTile * (kMaxFilters + 4);
+constexpr int kDctGroups = 4;  // phase 2b: waves 0..3, coefficients c = w, w+4, w+8, w+12
+
+// Phase 2a (runtime plan): frame `lane`, filters [fb, fe) -> log-mel row.
+__device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
+                                        const float* __restrict__ prow, int fb, int fe,
+                                        float* __restrict__ lrow) {
   const float eps = 0x1p-52f;  // np.finfo(float).eps, mfcc.py:74
-#pragma unroll
-  for (int c = 0; c < kMaxCoefs; ++c) acc[c] = 0.f;
   for (int m = fb; m < fe; ++m) {
     const int lo = plan->f_lo[m], n = plan->f_len[m];
     const float* w = plan->taps + plan->f_off[m];
@@ -203,100 +238,138 @@ __device__ __forceinline__ void mel_log_dct(const MfccDev* __restrict__ plan,
     for (; t < n; ++t) e0 = fmaf(w[t], pr[t], e0);
     float e = (e0 + e1) + (e2 + e3);
     e = (e == 0.f) ? eps : e;
-    const float lg = __log10f(e);
-#pragma unroll
-    for (int c = 0; c < kMaxCoefs; ++c) acc[c] = fmaf(plan->dct[c * kMaxFilters + m], lg, acc[c]);
+    lrow[m] = log10_pos(e);
   }
 }
 
-// log10 of a positive energy: native v_log_f32 (with a pre-scale for tiny
-// inputs) times log10(2) -- ~1e-7 relative, far inside the 1e-4 budget.
-__device__ __forceinline__ float log10_pos(float e) {
-  const bool tiny = e < 0x1p-100f;
-  const float x = tiny ? e * 0x1p64f : e;
-  const float l2 = __builtin_amdgcn_logf(x);  // log2
-  return fmaf(l2, 0.30102999566398120f, tiny ? -19.26591972249479649f : 0.f);
+// Phase 2b (runtime plan): lifter x DCT of one log-mel row for the
+// coefficients c = g + 4 i of group g.
+__device__ __forceinline__ void dct_rt(const MfccDev* __restrict__ plan,
+                                       const float* __restrict__ lrow, int g, int mfcc_n,
+                                       float (&acc)[4]) {
+  const int nf = plan->n_filters;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = g + kDctGroups * i;
+    float s0 = 0.f, s1 = 0.f;
+    if (c < mfcc_n) {
+      const float* d = plan->dct + c * kMaxFilters;
+      int m = 0;
+      for (; m + 1 < nf; m += 2) {
+        s0 = fmaf(d[m], lrow[m], s0);
+        s1 = fmaf(d[m + 1], lrow[m + 1], s1);
+      }
+      if (m < nf) s0 = fmaf(d[m], lrow[m], s0);
+    }
+    acc[i] = s0 + s1;
+  }
 }
 
-// Phase 2 specialised for a compile-time filterbank T (mel_tables.h): wave W
-// owns filters [band[W], band[W+1]); every bin of the band is read once from
-// the frame's LDS row as a 16-B vector and fed to its (at most two) filters
-// with literal weights; log10; partial lifter x DCT sums.
-// Phase 2 specialised for a compile-time filterbank T (mel_tables.h): wave W
-// owns filters [band[W], band[W+1]); every bin of its band is read once from
-// the frame's LDS row as a 16-B vector and fed to its (at most two) filters,
-// then log10 and the partial lifter x DCT sums.  The bodies are generated
-// (mel_code.h) as straight-line v_fmac_f32 with 32-bit literal weights.
+// Straight-line phase-2 code for a compile-time filterbank T (mel_tables.h),
+// generated into mel_code.h: mel_band_code<T, W> reads every bin of wave W's
+// filter band once from the frame's LDS power row as a 16-B vector, feeds it
+// to its (at most two) filters with literal weights and writes log10 of the
+// band's energies; dct_code<T, G> is the lifter x DCT of a log-mel row for
+// coefficient group G.
 template <class T, int W>
 __device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
-                                              float (&acc)[kMaxCoefs]);
+                                              float* __restrict__ lm);
+template <class T, int G>
+__device__ __forceinline__ void dct_code(const float* __restrict__ lm, float (&acc)[4]);
 
 #include "mel_code.h"
 
-template <class T, int W>
-__device__ __forceinline__ void mel_band(const float* __restrict__ prow, int z,
-                                         float (&acc)[kMaxCoefs]) {
-  (void)z;
-  mel_band_code<T, W>(static_cast<const float*>(__builtin_assume_aligned(prow, 16)), acc);
+template <class T>
+__device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float* lrow) {
+  prow = static_cast<const float*>(__builtin_assume_aligned(prow, 16));
+  switch (wave) {
+    case 0: mel_band_code<T, 0>(prow, lrow); break;
+    case 1: mel_band_code<T, 1>(prow, lrow); break;
+    case 2: mel_band_code<T, 2>(prow, lrow); break;
+    case 3: mel_band_code<T, 3>(prow, lrow); break;
+    case 4: mel_band_code<T, 4>(prow, lrow); break;
+    case 5: mel_band_code<T, 5>(prow, lrow); break;
+    case 6: mel_band_code<T, 6>(prow, lrow); break;
+    default: mel_band_code<T, 7>(prow, lrow); break;
+  }
 }
 
 template <class T>
-__device__ __forceinline__ void mel_dispatch(int wave, const float* prow, int z,
-                                             float (&acc)[kMaxCoefs]) {
-  switch (wave) {
-    case 0: mel_band<T, 0>(prow, z, acc); break;
-    case 1: mel_band<T, 1>(prow, z, acc); break;
-    case 2: mel_band<T, 2>(prow, z, acc); break;
-    case 3: mel_band<T, 3>(prow, z, acc); break;
-    case 4: mel_band<T, 4>(prow, z, acc); break;
-    case 5: mel_band<T, 5>(prow, z, acc); break;
-    case 6: mel_band<T, 6>(prow, z, acc); break;
-    default: mel_band<T, 7>(prow, z, acc); break;
+__device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&acc)[4]) {
+  lrow = static_cast<const float*>(__builtin_assume_aligned(lrow, 16));
+  switch (g) {
+    case 0: dct_code<T, 0>(lrow, acc); break;
+    case 1: dct_code<T, 1>(lrow, acc); break;
+    case 2: dct_code<T, 2>(lrow, acc); break;
+    default: dct_code<T, 3>(lrow, acc); break;
   }
 }
 
-constexpr int kPartStride = kMaxCoefs + 1;  // floats per (wave, frame) partial row
-
-// Phases 2 + 3 for one tile: mel / log / DCT partials per wave, summed
-// through LDS, coalesced store of the tile's MFCC rows.  SPEC 0 = runtime
-// plan, 1 = Mel26, 2 = Mel40 (compile-time tables).
+// Phase 2a: one frame per lane, wave `wave` owns a band of filters: mel
+// energies, (==0 -> eps), log10 into the tile's log-mel rows.
 template <int SPEC>
-__device__ __forceinline__ void tile_mfcc(const MfccDev* __restrict__ plan, const float* P,
-                                          float* part, int tid, int wave, int lane, int64_t f0,
-                                          int64_t n_frames, int mfcc_n_rt, float* __restrict__ out) {
+__device__ __forceinline__ void phase2a(const MfccDev* __restrict__ plan, const float* P,
+                                        float* lm, int wave, int lane) {
+  const float* prow = P + lane * kPStride;
+  float* lrow = lm + lane * lm_stride<SPEC>();
+  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
+  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
+  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
+}
+
+// Phase 2b (waves 0..3): lifter x DCT of the tile's log-mel rows, one frame
+// per lane, coefficients c = wave + 4 i, stored straight to the MFCC rows.
+template <int SPEC, bool STORE = true>
+__device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const float* lm,
+                                        int wave, int lane, int64_t f0, int64_t n_frames,
+                                        int mfcc_n_rt, float* __restrict__ out) {
   constexpr int NC = SPEC == 1 ? Mel26::NC : SPEC == 2 ? Mel40::NC : 0;
   const int mfcc_n = NC > 0 ? NC : mfcc_n_rt;
-  __syncthreads();
-  float acc[kMaxCoefs];
-  const int z = __builtin_amdgcn_readfirstlane((int)(f0 >> 48));  // 0, opaque per tile
-  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, P + lane * kPStride, z, acc);
-  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, P + lane * kPStride, z, acc);
-  else mel_log_dct(plan, P + lane * kPStride, plan->wave_fbeg[wave], plan->wave_fend[wave], acc);
+  const float* lrow = lm + lane * lm_stride<SPEC>();
+  float acc[4];
+  if constexpr (SPEC == 1) dct_dispatch<Mel26>(wave, lrow, acc);
+  else if constexpr (SPEC == 2) dct_dispatch<Mel40>(wave, lrow, acc);
+  else dct_rt(plan, lrow, wave, mfcc_n, acc);
+  const int64_t f = f0 + lane;
+  if constexpr (STORE) {
+    if (f < n_frames) {
+      float* o = out + f * mfcc_n;
 #pragma unroll
-  for (int c = 0; c < (NC > 0 ? NC : kMaxCoefs); ++c) part[(wave * 64 + lane) * kPartStride + c] = acc[c];
-  __syncthreads();
-  const int64_t nf = (n_frames - f0) < kTile ? (n_frames - f0) : kTile;
-  for (int i = tid; i < nf * mfcc_n; i += kThreads) {
-    const int lf = i / mfcc_n, c = i - lf * mfcc_n;
-    float s = 0.f;
-#pragma unroll
-    for (int w = 0; w < kWaves; ++w) s += part[(w * 64 + lf) * kPartStride + c];
-    out[f0 * mfcc_n + i] = s;
+      for (int i = 0; i < 4; ++i)
+        if (wave + kDctGroups * i < mfcc_n) o[wave + kDctGroups * i] = acc[i];
+    }
+  } else {
+    if (acc[0] == 12345.f) out[0] = acc[1] + acc[2] + acc[3];  // keep the work live
   }
-  __syncthreads();
 }
 
-// DIAG (diagnostic builds only, VAD_DIAG env): 1 = skip the FFT (phase 1
-// keeps its loads and P stores), 2 = skip phases 2-3, 3 = both (loads only),
-// 4 = FFT on register data without loads, no phases 2-3.  Outputs are wrong.
+// In-kernel timestamps for DIAG 5 (diagnostic build only): lane 0 of every
+// wave writes s_memtime at phase boundaries of its first 8 tiles into `out`
+// (the MFCC stores are suppressed).
+#define VAD_STAMP(k)                                                              \
+  do {                                                                            \
+    if constexpr (DIAG == 5) {                                                    \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
+      if (lane == 0 && it < 8)                                                    \
+        stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 8 + (k)] = t_;        \
+      __builtin_amdgcn_sched_barrier(0);                                          \
+    }                                                                             \
+  } while (0)
+
+constexpr size_t kPBytes = (size_t)kTile * kPStride * sizeof(float);          // 66,560
+constexpr size_t kScrBytes = (size_t)kGroups * kGroupScratch * sizeof(v2f);  // 73,728
+constexpr size_t kLmBytes = (size_t)kLmFloats * sizeof(float);               // 17,408
+
+// DIAG 5 (diagnostic build only, VAD_DIAG env): timestamps, outputs wrong.
 template <int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* P = reinterpret_cast<float*>(smem);                                   // [64][257]
-  v2f* scr = reinterpret_cast<v2f*>(smem + kTile * kPStride * sizeof(float));
-  float* part = reinterpret_cast<float*>(scr);            // phase 3 reuse: [wave][64][17]
+  float* P = reinterpret_cast<float*>(smem);                      // [64][260] power rows
+  v2f* scr = reinterpret_cast<v2f*>(smem + kPBytes);              // FFT transposes
+  float* lm = reinterpret_cast<float*>(smem + kPBytes + kScrBytes);  // [64][LMS] log-mel
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -318,7 +391,10 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // the taps carry the FFT path's 2^-20: undo it on true spectra (exact)
         P[lf * kPStride + k] = (f < n_frames) ? src[f * kBins + k] * 0x1p20f : 0.f;
       }
-      tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
+      __syncthreads();  // P complete; the previous tile's phase 2b is done
+      phase2a<SPEC>(plan, P, lm, wave, lane);
+      __syncthreads();  // log-mel rows complete; P free
+      if (wave < kDctGroups) phase2b<SPEC>(plan, lm, wave, lane, f0, n_frames, mfcc_n, out);
     }
   } else {
     v2f* gscr = scr + grp * kGroupScratch;
@@ -328,81 +404,91 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // the current pass computes
     v2f bufA[NZ], bufB[NZ];
     const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
-    int64_t tile = blockIdx.x;
-    {
-      int64_t f = tile * kTile + grp;
+    auto load_pass = [&](int64_t t, int pass, v2f (&buf)[NZ]) {
+      int64_t f = t * kTile + pass * kGroups + grp;
       f = f < flast ? f : flast;
-      load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
-    }
-    for (; tile < n_tiles; tile += gridDim.x) {
+      load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, buf);
+    };
+    int64_t tile = blockIdx.x;
+    load_pass(tile, 0, bufA);
+    load_pass(tile, 1, bufB);
+    unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
+    int it = 0;
+    (void)stamps;
+    int64_t prev_f0 = -1;  // tile whose log-mel rows await phase 2b
+    // Per tile and wave: two passes of 4 frames.  Each pass's samples are
+    // loaded one tile ahead, right after its stage A consumed the previous
+    // ones; pass 1's stage A runs while pass 0's transpose reads are in
+    // flight.  sched_barriers pin that order (the scheduler would otherwise
+    // hoist the loads or sink the reads).
+    for (; tile < n_tiles; tile += gridDim.x, ++it) {
       const int64_t f0 = tile * kTile;
-      {  // prefetch pass 1 of this tile
-        int64_t f = f0 + kGroups + grp;
-        f = f < flast ? f : flast;
-        if constexpr (DIAG == 4) {
-#pragma unroll
-          for (int n = 0; n < NZ; ++n) bufB[n] = (v2f){(float)(f + n), (float)(j - n)};
-        } else {
-          load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufB);
-        }
+      const int64_t fa = f0 + grp, fb = f0 + kGroups + grp;
+      float* prow_a;
+      float* prow_b;
+      if constexpr (MODE == kAudioToSpec) {
+        prow_a = out + (fa < n_frames ? fa : flast) * kBins;
+        prow_b = out + (fb < n_frames ? fb : flast) * kBins;
+      } else {
+        prow_a = P + grp * kPStride;
+        prow_b = P + (kGroups + grp) * kPStride;
       }
-      // keep the scheduler from hoisting the next pass's FFT above this
-      // pass (that would wait on the loads just issued and defeat the
-      // prefetch distance)
+      VAD_STAMP(0);
+      v2f u[16], col[32];
+      stage_a<NZ, LEN>(bufA, len, L, j, u);
       __builtin_amdgcn_sched_barrier(0);
-      {  // pass 0
-        const int64_t f = f0 + grp;
-        if constexpr (MODE == kAudioToSpec) {
-          if (f < n_frames) frame_power<NZ, LEN, true>(bufA, len, L, j, gscr, out + f * kBins);
-        } else {
-          if constexpr (DIAG == 1 || DIAG == 3) {
-            P[grp * kPStride + j] = bufA[j % NZ].x + bufA[(j + 5) % NZ].y;
-          } else {
-            frame_power<NZ, LEN, false>(bufA, len, L, j, gscr, P + grp * kPStride);
-          }
-        }
-      }
+      load_pass(tile + gridDim.x, 0, bufA);
       __builtin_amdgcn_sched_barrier(0);
-      {  // prefetch pass 0 of the next tile
-        int64_t f = (tile + gridDim.x) * kTile + grp;
-        f = f < flast ? f : flast;
-        if constexpr (DIAG == 4) {
-#pragma unroll
-          for (int n = 0; n < NZ; ++n) bufA[n] = (v2f){(float)(f - n), (float)(j + n)};
-        } else {
-          load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, bufA);
-        }
+      store_a(u, gscr, j);
+      read_b(L, gscr, col);
+      if constexpr (LEN > 0) {
+        // overlap: pass 1's stage A covers the latency of pass 0's reads
+        __builtin_amdgcn_sched_barrier(0);
+        stage_a<NZ, LEN>(bufB, len, L, j, u);
+        __builtin_amdgcn_sched_barrier(0);
+        load_pass(tile + gridDim.x, 1, bufB);
+        __builtin_amdgcn_sched_barrier(0);
+        if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+      } else {
+        // runtime frame length: the sequential order keeps the generic
+        // variants within 256 VGPRs
+        if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_a<NZ, LEN>(bufB, len, L, j, u);
+        __builtin_amdgcn_sched_barrier(0);
+        load_pass(tile + gridDim.x, 1, bufB);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
-      {  // pass 1
-        const int64_t f = f0 + kGroups + grp;
-        if constexpr (MODE == kAudioToSpec) {
-          if (f < n_frames) frame_power<NZ, LEN, true>(bufB, len, L, j, gscr, out + f * kBins);
-        } else {
-          if constexpr (DIAG == 1 || DIAG == 3) {
-            P[(kGroups + grp) * kPStride + j] = bufB[j % NZ].x + bufB[(j + 5) % NZ].y;
-          } else {
-            frame_power<NZ, LEN, false>(bufB, len, L, j, gscr, P + (kGroups + grp) * kPStride);
-          }
-        }
+      VAD_STAMP(1);
+      store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
+      read_b(L, gscr, col);
+      if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+      if constexpr (MODE == kAudioToMfcc) {
+        __builtin_amdgcn_sched_barrier(0);
+        VAD_STAMP(2);
+        // the previous tile's DCT runs on the waves that finish phase 1
+        // first (waves 0..3 are older and win VALU arbitration on their
+        // SIMD) while their SIMD partners are still in their FFT
+        if (prev_f0 >= 0 && wave < kDctGroups)
+          phase2b<SPEC, DIAG != 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        VAD_STAMP(3);
+        __syncthreads();  // P complete; log-mel rows consumed
+        VAD_STAMP(4);
+        phase2a<SPEC>(plan, P, lm, wave, lane);
+        VAD_STAMP(5);
+        __syncthreads();  // log-mel rows complete; P and the FFT scratch free
+        VAD_STAMP(6);
+        prev_f0 = f0;
       }
-      if constexpr (MODE == kAudioToMfcc && DIAG <= 1)
-        tile_mfcc<SPEC>(plan, P, part, tid, wave, lane, f0, n_frames, mfcc_n, out);
-      if constexpr (DIAG >= 2) {
-        __syncthreads();
-        if (tid < 64) out[f0 * 13 + tid] = P[tid * kPStride + (tid & 15)];
-        __syncthreads();
-      }
+    }
+    if constexpr (MODE == kAudioToMfcc) {
+      if (prev_f0 >= 0 && wave < kDctGroups)
+        phase2b<SPEC, DIAG != 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
 
-size_t mfcc_smem_bytes() {
-  const size_t p = kTile * kPStride * sizeof(float);  // 65792 B, 16-B multiple
-  const size_t s = kGroups * kGroupScratch * sizeof(v2f);
-  const size_t part = kWaves * 64 * kPartStride * sizeof(float);
-  return p + (s > part ? s : part);
-}
+size_t mfcc_smem_bytes() { return kPBytes + kScrBytes + kLmBytes; }  // 157,696 B
 
 static int num_cus() {
   static int n = 0;
@@ -443,10 +529,7 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const float* src, int6
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
-      if (diag == 1) return launch_t<MODE, 13, true, 400, 1, 1>(plan, src, stride, len, n, out, st);
-      if (diag == 2) return launch_t<MODE, 13, true, 400, 1, 2>(plan, src, stride, len, n, out, st);
-      if (diag == 3) return launch_t<MODE, 13, true, 400, 1, 3>(plan, src, stride, len, n, out, st);
-      if (diag == 4) return launch_t<MODE, 13, true, 400, 1, 4>(plan, src, stride, len, n, out, st);
+      if (diag == 5) return launch_t<MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
       return launch_t<MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2)

@@ -26,7 +26,9 @@ CONFIGS = [
     ("Mel26", 300, 8000, 26, 16000, 13, 22),   # config.py:20-27, sklearn_analyser.py:21
     ("Mel40", 300, 8000, 40, 16000, 13, 22),   # BASELINE.json config 2
 ]
-WAVES = 8
+WAVES = 8          # phase-2a filter bands (one per wave)
+DCT_GROUPS = 4     # phase-2b coefficient groups c = g, g+4, ... (waves 0..3)
+DCT_PER_GROUP = 4
 
 
 def mel_filterbank(lo, hi, nf, sr, fft_n=512):
@@ -76,7 +78,7 @@ def emit(name, lo, hi, nf, sr, nc, L):
     dense = np.zeros((nf, 256), np.float32)
     for m in range(nf):
         dense[m, los[m]:los[m] + lens[m]] = taps[m]
-    cost = [lens[m] + 2 * nc + 8 for m in range(nf)]
+    cost = [lens[m] + 8 for m in range(nf)]  # taps + (==0 -> eps) + log10
     total = sum(cost)
     band, acc, m = [0], 0, 0
     for w in range(WAVES):
@@ -111,20 +113,21 @@ def bits(x):
 
 
 def emit_code(name, info):
-    """Straight-line phase-2 code per wave band: one v_fmac_f32 with a
-    32-bit literal per tap / DCT term (VOP2 literal: no SGPR, nothing for the
-    compiler to hoist out of the persistent tile loop and spill)."""
+    """Straight-line phase-2 code: per wave band the mel energies and their
+    log10 (mel_band_code), per coefficient group the lifter x DCT of a frame's
+    log-mel row (dct_code).  One v_fmac_f32 with a 32-bit literal per tap /
+    DCT term (VOP2 literal: no SGPR, nothing for the compiler to hoist out of
+    the persistent tile loop and spill)."""
     los, lens, taps, d, band, dense = info
     nf, nc = d.shape[1], d.shape[0]
     out = []
+    comp = "xyzw"
     for w in range(WAVES):
         fb, fe = band[w], band[w + 1]
         out.append(f"template <> __device__ __forceinline__ void mel_band_code<{name}, {w}>(")
-        out.append("    const float* __restrict__ prow, float (&acc)[kMaxCoefs]) {")
+        out.append("    const float* __restrict__ prow, float* __restrict__ lm) {")
         if fb == fe:
-            out.append("  (void)prow;")
-            out.append("#pragma unroll\n  for (int c = 0; c < kMaxCoefs; ++c) acc[c] = 0.f;")
-            out.append("}")
+            out.append("  (void)prow;\n  (void)lm;\n}")
             continue
         k0 = los[fb] & ~3
         k1 = los[fe - 1] + lens[fe - 1]
@@ -132,7 +135,6 @@ def emit_code(name, info):
         for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
                        f"__builtin_assume_aligned(prow + {k0 + 4 * q}, 16));")
-        comp = "xyzw"
         first = {}
         for m in range(fb, fe):
             out.append(f"  float e{m - fb};")
@@ -149,16 +151,31 @@ def emit_code(name, info):
                     out.append(f'  asm("v_mul_f32_e32 %0, {bits(v)}, %1" : "=v"({reg}) : "v"({src}));')
                 else:
                     out.append(f'  asm("v_fmac_f32_e32 %0, {bits(v)}, %1" : "+v"({reg}) : "v"({src}));')
-        for c in range(nc):
-            out.append(f"  acc[{c}] = 0.f;")
-        for c in range(nc, 16):
-            out.append(f"  acc[{c}] = 0.f;")
         for m in range(fb, fe):
-            out.append(f"  {{  // filter {m}: (==0 -> eps), log10, lifter x DCT column")
-            out.append(f"    const float lg = log10_pos(e{m - fb} == 0.f ? 0x1p-52f : e{m - fb});")
-            for c in range(nc):
-                out.append(f'    asm("v_fmac_f32_e32 %0, {bits(d[c, m])}, %1" : "+v"(acc[{c}]) : "v"(lg));')
-            out.append("  }")
+            out.append(f"  lm[{m}] = log10_pos(e{m - fb} == 0.f ? 0x1p-52f : e{m - fb});"
+                       f"  // (==0 -> eps), log10")
+        out.append("}")
+        out.append("")
+    nq = (nf + 3) // 4
+    for g in range(DCT_GROUPS):
+        coefs = list(range(g, nc, DCT_GROUPS))
+        out.append(f"template <> __device__ __forceinline__ void dct_code<{name}, {g}>(")
+        out.append(f"    const float* __restrict__ lm, float (&acc)[{DCT_PER_GROUP}]) {{")
+        for q in range(nq):
+            out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
+                       f"__builtin_assume_aligned(lm + {4 * q}, 16));")
+        for i, c in enumerate(coefs):
+            out.append(f"  float a{i}, b{i};  // coefficient {c}: even / odd filters")
+            for m in range(nf):
+                reg = f"a{i}" if m % 2 == 0 else f"b{i}"
+                q, r = divmod(m, 4)
+                src = f"q{q}.{comp[r]}"
+                if m < 2:
+                    out.append(f'  asm("v_mul_f32_e32 %0, {bits(d[c, m])}, %1" : "=v"({reg}) : "v"({src}));')
+                else:
+                    out.append(f'  asm("v_fmac_f32_e32 %0, {bits(d[c, m])}, %1" : "+v"({reg}) : "v"({src}));')
+        for i in range(DCT_PER_GROUP):
+            out.append(f"  acc[{i}] = a{i} + b{i};" if i < len(coefs) else f"  acc[{i}] = 0.f;")
         out.append("}")
         out.append("")
     return "\n".join(out)
@@ -170,9 +187,10 @@ def main():
              "// configurations (mfcc.py:39-56, 72-93; config.py:20-27).",
              "#pragma once", "", "namespace vad {", ""]
     code = ["// GENERATED by vad_amd/gen_tables.py -- do not edit.",
-            "// Straight-line phase-2 (mel / log10 / lifter x DCT) code per wave band",
-            "// for the compile-time filterbanks of mel_tables.h.  Included by",
-            "// mfcc_kernel.hip after mel_band_code / log10_pos are declared.",
+            "// Straight-line phase-2 code for the compile-time filterbanks of",
+            "// mel_tables.h: mel / log10 per wave band (phase 2a) and lifter x DCT",
+            "// per coefficient group (phase 2b).  Included by mfcc_kernel.hip after",
+            "// mel_band_code / dct_code / log10_pos are declared.",
             "#pragma once", ""]
     for cfg in CONFIGS:
         src, info = emit(*cfg)
