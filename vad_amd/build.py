@@ -17,6 +17,14 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvad_amd.so")
 ARCH = os.environ.get("VAD_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["capi.hip", "mfcc_kernel.hip", "ffn_kernel.hip"]
+# per-translation-unit code-generation flags: the FFT's packed-fp32 chains
+# run ~5% faster under the ILP-oriented machine scheduler (fewer dependent
+# pairs back to back, i.e. fewer hazard s_nops and stalls)
+UNIT_FLAGS = {
+    "mfcc_kernel.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "ffn_kernel.hip": [],
+    "capi.hip": [],
+}
 
 
 def sources():
@@ -37,12 +45,25 @@ def build(force=False, verbose=True):
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-Wno-unused-function", "-o", LIB + ".tmp"] + sources()
+    base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
+            "-Wno-unused-function"]
+    procs, objs = [], []
+    for name in SOURCES:  # one object per unit, compiled in parallel
+        obj = os.path.join(LIB_DIR, name.replace(".hip", ".o"))
+        cmd = base + UNIT_FLAGS.get(name, []) + ["-c", os.path.join(CSRC, name), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc -c")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    for obj in objs:
+        os.remove(obj)
     return LIB
 
 
