@@ -6,7 +6,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["VAD_DIAG"] = "5"
+os.environ.setdefault("VAD_DIAG", "5")
 from bench import synth_audio  # noqa: E402
 from vad_amd.pipeline import VadPipeline  # noqa: E402
 
@@ -17,14 +17,13 @@ out = torch.zeros((F, 13), dtype=torch.float32, device="cuda")
 for _ in range(3):
     pipe.mfcc(audio, out=out)
 torch.cuda.synchronize()
-st = out.reshape(-1).view(torch.int64)[: 256 * 8 * 8 * 8].cpu().numpy().reshape(256, 8, 8, 8)
-st = st[:, :, 1:7, :]  # skip first tile (cold), keep iterations 1..6
-d = np.diff(st[..., :7].astype(np.float64), axis=-1)  # 6 intervals
-names = ["pass0", "pass1", "phase2b", "bar1", "phase2a", "bar2"]
-tot = d.sum(axis=-1)
-print("cycles per tile (median over blocks/waves/iters):", np.median(tot))
+st = out.reshape(-1).view(torch.int64)[: 256 * 8 * 8 * 16].cpu().numpy().reshape(256, 8, 8, 16)
+waves = range(8) if os.environ["VAD_DIAG"] == "5" else range(4)
+st = st[:, list(waves), 1:7, :11]  # skip the first tile (cold), keep tiles 1..6
+d = np.diff(st.astype(np.float64), axis=-1)  # 10 intervals
+names = ["stageA_A", "xposeA", "stageA_B", "finish_A", "xposeB", "finish_B", "phase2b", "bar1",
+         "phase2a", "bar2"]
+tot = np.median(st[..., 10] - st[..., 0])
+print(f"VAD_DIAG={os.environ['VAD_DIAG']}: median cycles per tile {tot:.0f}")
 for i, n in enumerate(names):
-    print(f"{n:8s} median {np.median(d[..., i]):8.0f}  mean {d[..., i].mean():8.0f}  "
-          f"share {d[..., i].mean() / tot.mean():.3f}")
-for i, n in enumerate(names):
-    print(f"per-wave {n} medians:", [int(np.median(d[:, w, :, i])) for w in range(8)])
+    print(f"{n:9s}", [int(np.median(d[:, w, :, i])) for w in range(len(waves))])

@@ -343,25 +343,27 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
   }
 }
 
-// In-kernel timestamps for DIAG 5 (diagnostic build only): lane 0 of every
-// wave writes s_memtime at phase boundaries of its first 8 tiles into `out`
-// (the MFCC stores are suppressed).
+// In-kernel timestamps for DIAG 5/6 (diagnostic builds only): every wave
+// takes s_memtime at phase boundaries into SGPRs; lane 0 stores them at the
+// end of each of its first 8 tiles into `out` as [block][wave][tile][16]
+// (deferred, so that the stamps add no lgkmcnt waits inside the tile; the
+// MFCC stores are suppressed).  DIAG 6 idles waves 4..7 (barriers only) to
+// time the older waves' phases alone.
 #define VAD_STAMP(k)                                                              \
   do {                                                                            \
-    if constexpr (DIAG == 5) {                                                    \
+    if constexpr (DIAG >= 5) {                                                    \
       __builtin_amdgcn_sched_barrier(0);                                          \
-      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                \
-      if (lane == 0 && it < 8)                                                    \
-        stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 8 + (k)] = t_;        \
+      st_[k] = __builtin_amdgcn_s_memtime();                                      \
       __builtin_amdgcn_sched_barrier(0);                                          \
     }                                                                             \
   } while (0)
+constexpr int kStamps = 11;
 
 constexpr size_t kPBytes = (size_t)kTile * kPStride * sizeof(float);          // 66,560
 constexpr size_t kScrBytes = (size_t)kGroups * kGroupScratch * sizeof(v2f);  // 73,728
 constexpr size_t kLmBytes = (size_t)kLmFloats * sizeof(float);               // 17,408
 
-// DIAG 5 (diagnostic build only, VAD_DIAG env): timestamps, outputs wrong.
+// DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
 template <int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
@@ -433,57 +435,74 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         prow_a = P + grp * kPStride;
         prow_b = P + (kGroups + grp) * kPStride;
       }
+      unsigned long long st_[kStamps];
+      (void)st_;
+      // DIAG 6: waves 4..7 skip all work but the barriers
+      const bool work = DIAG != 6 || wave < 4;
       VAD_STAMP(0);
       v2f u[16], col[32];
-      stage_a<NZ, LEN>(bufA, len, L, j, u);
-      __builtin_amdgcn_sched_barrier(0);
-      load_pass(tile + gridDim.x, 0, bufA);
-      __builtin_amdgcn_sched_barrier(0);
-      store_a(u, gscr, j);
-      read_b(L, gscr, col);
-      if constexpr (LEN > 0) {
-        // overlap: pass 1's stage A covers the latency of pass 0's reads
+      if (work) {
+        stage_a<NZ, LEN>(bufA, len, L, j, u);
+        VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
-        stage_a<NZ, LEN>(bufB, len, L, j, u);
+        load_pass(tile + gridDim.x, 0, bufA);
         __builtin_amdgcn_sched_barrier(0);
-        load_pass(tile + gridDim.x, 1, bufB);
-        __builtin_amdgcn_sched_barrier(0);
-        if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
-      } else {
-        // runtime frame length: the sequential order keeps the generic
-        // variants within 256 VGPRs
-        if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
-        __builtin_amdgcn_sched_barrier(0);
-        stage_a<NZ, LEN>(bufB, len, L, j, u);
-        __builtin_amdgcn_sched_barrier(0);
-        load_pass(tile + gridDim.x, 1, bufB);
-        __builtin_amdgcn_sched_barrier(0);
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
+        if constexpr (LEN > 0) {
+          // overlap: pass 1's stage A covers the latency of pass 0's reads
+          __builtin_amdgcn_sched_barrier(0);
+          VAD_STAMP(2);
+          stage_a<NZ, LEN>(bufB, len, L, j, u);
+          __builtin_amdgcn_sched_barrier(0);
+          load_pass(tile + gridDim.x, 1, bufB);
+          __builtin_amdgcn_sched_barrier(0);
+          VAD_STAMP(3);
+          if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+        } else {
+          // runtime frame length: the sequential order keeps the generic
+          // variants within 256 VGPRs
+          if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+          __builtin_amdgcn_sched_barrier(0);
+          stage_a<NZ, LEN>(bufB, len, L, j, u);
+          __builtin_amdgcn_sched_barrier(0);
+          load_pass(tile + gridDim.x, 1, bufB);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        VAD_STAMP(4);
+        store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
+        read_b(L, gscr, col);
+        VAD_STAMP(5);
+        if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
       }
-      VAD_STAMP(1);
-      store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
-      read_b(L, gscr, col);
-      if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
       if constexpr (MODE == kAudioToMfcc) {
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(2);
+        VAD_STAMP(6);
         // the previous tile's DCT runs on the waves that finish phase 1
         // first (waves 0..3 are older and win VALU arbitration on their
         // SIMD) while their SIMD partners are still in their FFT
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG != 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
-        VAD_STAMP(3);
+          phase2b<SPEC, DIAG < 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        VAD_STAMP(7);
         __syncthreads();  // P complete; log-mel rows consumed
-        VAD_STAMP(4);
-        phase2a<SPEC>(plan, P, lm, wave, lane);
-        VAD_STAMP(5);
+        VAD_STAMP(8);
+        if (work) phase2a<SPEC>(plan, P, lm, wave, lane);
+        VAD_STAMP(9);
         __syncthreads();  // log-mel rows complete; P and the FFT scratch free
-        VAD_STAMP(6);
+        VAD_STAMP(10);
         prev_f0 = f0;
+        if constexpr (DIAG >= 5) {
+          if (lane == 0 && it < 8) {
+#pragma unroll
+            for (int k = 0; k < kStamps; ++k)
+              stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 16 + k] = st_[k];
+          }
+        }
       }
     }
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG != 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b<SPEC, DIAG < 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -530,6 +549,7 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const float* src, int6
     if (MODE == kAudioToMfcc && spec == 1) {
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
       if (diag == 5) return launch_t<MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 6) return launch_t<MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
       return launch_t<MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2)

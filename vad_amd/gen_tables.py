@@ -135,22 +135,32 @@ def emit_code(name, info):
         for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
                        f"__builtin_assume_aligned(prow + {k0 + 4 * q}, 16));")
-        first = {}
+        # each filter's taps split into two interleaved sub-chains, all chains
+        # of the band emitted round-robin (volatile: the order is the issue
+        # order), so that no fmac consumes the accumulator written by the
+        # instruction just before it -- more ILP and no hazard s_nops
+        chains = []
         for m in range(fb, fe):
-            out.append(f"  float e{m - fb};")
-        for k in range(k0, k1):
-            q, r = divmod(k - k0, 4)
-            for m in range(fb, fe):
-                v = dense[m, k]
-                if v == 0:
+            tp = [(k, dense[m, k]) for k in range(k0, k1) if dense[m, k] != 0]
+            halves = [tp[0::2], tp[1::2]] if len(tp) >= 4 else [tp]
+            for h, t in enumerate(halves):
+                chains.append((f"e{m - fb}_{h}", t))
+        for reg, _ in chains:
+            out.append(f"  float {reg};")
+        for step in range(max(len(t) for _, t in chains)):
+            for reg, t in chains:
+                if step >= len(t):
                     continue
-                reg = f"e{m - fb}"
+                k, v = t[step]
+                q, r = divmod(k - k0, 4)
                 src = f"q{q}.{comp[r]}"
-                if m not in first:
-                    first[m] = True
-                    out.append(f'  asm("v_mul_f32_e32 %0, {bits(v)}, %1" : "=v"({reg}) : "v"({src}));')
+                if step == 0:
+                    out.append(f'  asm volatile("v_mul_f32_e32 %0, {bits(v)}, %1" : "=v"({reg}) : "v"({src}));')
                 else:
-                    out.append(f'  asm("v_fmac_f32_e32 %0, {bits(v)}, %1" : "+v"({reg}) : "v"({src}));')
+                    out.append(f'  asm volatile("v_fmac_f32_e32 %0, {bits(v)}, %1" : "+v"({reg}) : "v"({src}));')
+        for m in range(fb, fe):
+            regs = [reg for reg, _ in chains if reg.startswith(f"e{m - fb}_")]
+            out.append(f"  const float e{m - fb} = {' + '.join(regs)};")
         for m in range(fb, fe):
             out.append(f"  lm[{m}] = log10_pos(e{m - fb} == 0.f ? 0x1p-52f : e{m - fb});"
                        f"  // (==0 -> eps), log10")
@@ -164,16 +174,20 @@ def emit_code(name, info):
         for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
                        f"__builtin_assume_aligned(lm + {4 * q}, 16));")
+        chains = []  # (register, coefficient, filter parity)
         for i, c in enumerate(coefs):
             out.append(f"  float a{i}, b{i};  // coefficient {c}: even / odd filters")
-            for m in range(nf):
-                reg = f"a{i}" if m % 2 == 0 else f"b{i}"
+            chains += [(f"a{i}", c, 0), (f"b{i}", c, 1)]
+        for step in range((nf + 1) // 2):
+            for reg, c, par in chains:
+                m = 2 * step + par
+                if m >= nf:
+                    continue
                 q, r = divmod(m, 4)
                 src = f"q{q}.{comp[r]}"
-                if m < 2:
-                    out.append(f'  asm("v_mul_f32_e32 %0, {bits(d[c, m])}, %1" : "=v"({reg}) : "v"({src}));')
-                else:
-                    out.append(f'  asm("v_fmac_f32_e32 %0, {bits(d[c, m])}, %1" : "+v"({reg}) : "v"({src}));')
+                op = "v_mul_f32_e32" if step == 0 else "v_fmac_f32_e32"
+                cons = "=v" if step == 0 else "+v"
+                out.append(f'  asm volatile("{op} %0, {bits(d[c, m])}, %1" : "{cons}"({reg}) : "v"({src}));')
         for i in range(DCT_PER_GROUP):
             out.append(f"  acc[{i}] = a{i} + b{i};" if i < len(coefs) else f"  acc[{i}] = 0.f;")
         out.append("}")
