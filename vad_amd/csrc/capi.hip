@@ -236,6 +236,16 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   for (int l = 0; l < n_layers; ++l)
     for (int mt = 0; mt < tiles[l]; ++mt)
       for (int r = 0; r < 4; ++r) push_slot([&](int g, int) { return b_at(l, 16 * mt + 4 * g + r); });
+  // output layer on the VALU (kernels' Topo::VL: >= 2 input tiles): slot
+  // (c*TIL + t)*4 + r -> W_last[16t + 4g + r][c] for 4 classes, then b_last[c]
+  if (n_layers >= 2 && tiles[n_layers - 2] >= 2) {
+    const int l = n_layers - 1, til = tiles[n_layers - 2];
+    for (int c = 0; c < 4; ++c)
+      for (int t = 0; t < til; ++t)
+        for (int r = 0; r < 4; ++r)
+          push_slot([&](int g, int) { return w_at(l, 16 * t + 4 * g + r, c); });
+    for (int c = 0; c < 4; ++c) push_slot([&](int, int) { return b_at(l, c); });
+  }
 
   vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));
   if (!p) return VAD_ENOMEM;

@@ -121,22 +121,81 @@ __device__ __forceinline__ void dense_layer(const float* __restrict__ a, const f
 }
 
 // Network shape: KS0 layer-0 K-steps (4 features each), Tl = 16-row output
-// tiles of layer l (0 = absent).  The last present layer has one tile.
-template <int KS0, int T1, int T2, int T3, int T4>
+// tiles of layer l (0 = absent); the last present layer has one tile.  NC =
+// classes the argmax reads (<= 4).  VL: the output layer runs on the VALU
+// when its input spans >= 2 tiles -- a 16-row MFMA tile would waste 16-NC of
+// its rows (13-64-64-2: 16 MFMAs per 16 windows become 32 FMAs per lane and a
+// cross-lane sum).
+template <int KS0, int T1, int T2, int T3, int T4, int NC = 4>
 struct Topo {
   static constexpr int NL = (T1 > 0) + (T2 > 0) + (T3 > 0) + (T4 > 0);
+  static constexpr int TIL = NL == 2 ? T1 : NL == 3 ? T2 : NL == 4 ? T3 : 0;  // last layer's input tiles
+  static constexpr bool VL = NL >= 2 && TIL >= 2;
   static constexpr int A0 = T1 * KS0;
   static constexpr int A1 = T2 * T1 * 4;
   static constexpr int A2 = T3 * T2 * 4;
   static constexpr int A3 = T4 * T3 * 4;
-  static constexpr int NA = A0 + A1 + A2 + A3;
+  static constexpr int NA_ALL = A0 + A1 + A2 + A3;
+  static constexpr int A_LAST = NL == 1 ? A0 : NL == 2 ? A1 : NL == 3 ? A2 : A3;
   static constexpr int NB = 4 * (T1 + T2 + T3 + T4);
+  // slots the kernel keeps in VGPRs: the output layer's MFMA A operands are
+  // skipped when it runs on the VALU (they stay in the fragment array)
+  static constexpr int NA = VL ? NA_ALL - A_LAST : NA_ALL;
+  // VALU output layer: after the A and bias slots, slot (c*TIL + t)*4 + r ->
+  // W_last[16t + 4g + r][c] (4 classes), then 4 slots of b_last[c]
+  static constexpr int NV = VL ? NC * TIL * 4 : 0;
+  static constexpr int NVB = VL ? NC : 0;
 };
 
-template <int KS0, int T1, int T2, int T3, int T4>
+// Load the per-lane weight fragments a network keeps in VGPRs.
+template <class TP>
+__device__ __forceinline__ void load_frags(const float* __restrict__ frag, int lane, float (&fa)[TP::NA],
+                                           float (&fb)[TP::NB], float (&fv)[TP::NV + TP::NVB + 1]) {
+#pragma unroll
+  for (int s = 0; s < TP::NA; ++s) fa[s] = frag[s * 64 + lane];
+#pragma unroll
+  for (int s = 0; s < TP::NB; ++s) fb[s] = frag[(TP::NA_ALL + s) * 64 + lane];
+  constexpr int v0 = TP::NA_ALL + TP::NB;
+  constexpr int ncl = TP::VL ? TP::NV / (TP::TIL * 4) : 0;
+#pragma unroll
+  for (int c = 0; c < ncl; ++c)
+#pragma unroll
+    for (int q = 0; q < TP::TIL * 4; ++q) fv[c * TP::TIL * 4 + q] = frag[(v0 + c * TP::TIL * 4 + q) * 64 + lane];
+#pragma unroll
+  for (int c = 0; c < TP::NVB; ++c) fv[TP::NV + c] = frag[(v0 + 4 * TP::TIL * 4 + c) * 64 + lane];
+  fv[TP::NV + TP::NVB] = 0.f;
+}
+
+// VALU output layer: lane (g, window jw) holds hidden units 16t + 4g + r of
+// its window; each class is a 16-term partial sum per lane, completed across
+// the four lane groups (xor 16, xor 32: a fixed association, deterministic).
+template <class TP, int TI>
+__device__ __forceinline__ f32x4 valu_out_layer(const float* __restrict__ fv, const f32x4 (&h)[TI]) {
+  constexpr int NC = TP::NVB;
+  f32x4 z = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int t = 0; t < TI; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        p0 = fmaf(fv[(c * TI + t) * 4 + r], h[t][r], p0);
+        p1 = fmaf(fv[(c * TI + t) * 4 + r + 1], h[t][r + 1], p1);
+      }
+    }
+    float p = p0 + p1;
+    p += __shfl_xor(p, 16);
+    p += __shfl_xor(p, 32);
+    z[c] = p + fv[TP::NV + c];
+  }
+  return z;
+}
+
+template <int KS0, int T1, int T2, int T3, int T4, int NC>
 __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const float* __restrict__ fb,
-                                             const float (&x)[KS0]) {
-  using TP = Topo<KS0, T1, T2, T3, T4>;
+                                             const float* __restrict__ fv, const float (&x)[KS0]) {
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   f32x4 h1[T1];
 #pragma unroll
   for (int mt = 0; mt < T1; ++mt) h1[mt] = (f32x4){fb[mt * 4 + 0], fb[mt * 4 + 1], fb[mt * 4 + 2], fb[mt * 4 + 3]};
@@ -156,14 +215,17 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
   }
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (TP::NL == 1) return h1[0];
+  else if constexpr (TP::NL == 2 && TP::VL) return valu_out_layer<TP, T1>(fv, h1);
   else {
     f32x4 h2[T2];
     dense_layer<T2, T1>(fa + TP::A0, fb + 4 * T1, h1, h2, TP::NL > 2);
     if constexpr (TP::NL == 2) return h2[0];
+    else if constexpr (TP::NL == 3 && TP::VL) return valu_out_layer<TP, T2>(fv, h2);
     else {
       f32x4 h3[T3];
       dense_layer<T3, T2>(fa + TP::A0 + TP::A1, fb + 4 * (T1 + T2), h2, h3, TP::NL > 3);
       if constexpr (TP::NL == 3) return h3[0];
+      else if constexpr (TP::VL) return valu_out_layer<TP, T3>(fv, h3);
       else {
         f32x4 h4[T4];
         dense_layer<T4, T3>(fa + TP::A0 + TP::A1 + TP::A2, fb + 4 * (T1 + T2 + T3), h3, h4, false);
@@ -177,11 +239,11 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
 enum Src { kFromMfcc = 0, kFromRows = 1 };
 
 // One wave per 16-window tile, persistent over tiles.
-template <int KS0, int T1, int T2, int T3, int T4, int SRC>
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int SRC>
 __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __restrict__ in,
                                                   int64_t n_rows, int mfcc_n, int mode,
                                                   uint8_t* __restrict__ labels) {
-  using TP = Topo<KS0, T1, T2, T3, T4>;
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int jw = lane & 15;
@@ -189,10 +251,8 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 
   float fa[TP::NA];
   float fb[TP::NB];
-#pragma unroll
-  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
-#pragma unroll
-  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+  float fv[TP::NV + TP::NVB + 1];
+  load_frags<TP>(net.frag, lane, fa, fb, fv);
 
   const int64_t n_tiles = (n_rows + 15) / 16;
   const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -216,7 +276,7 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
       }
       x[s] = v;
     }
-    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     if (g == 0 && valid) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
   }
 }
@@ -230,11 +290,11 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 constexpr int kChunk = 64;
 constexpr int kXStride = 65;  // floats per feature row (64 + 1: bank spread)
 
-template <int KS0, int T1, int T2, int T3, int T4, int MN>
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN>
 __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float* __restrict__ mfcc,
                                                          int64_t n_rows, int mfcc_n_rt, int mode,
                                                          uint8_t* __restrict__ labels) {
-  using TP = Topo<KS0, T1, T2, T3, T4>;
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   __shared__ float rows[(kChunk + 4) * kMaxCoefs];
   __shared__ float X[kChunk * kXStride];
   const int mfcc_n = MN > 0 ? MN : mfcc_n_rt;
@@ -248,10 +308,8 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
 
   float fa[TP::NA];
   float fb[TP::NB];
-#pragma unroll
-  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
-#pragma unroll
-  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+  float fv[TP::NV + TP::NVB + 1];
+  load_frags<TP>(net.frag, lane, fa, fb, fv);
 
   const int64_t n_frames = n_rows + 5;
   const int64_t n_chunks = (n_rows + kChunk - 1) / kChunk;
@@ -306,7 +364,7 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
       const int f = 4 * s + g;
       x[s] = (f < in_dim && f < nfeat && wl < nwin) ? X[wl * kXStride + f] : 0.f;
     }
-    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     if (g == 0 && wl < nwin) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
     __syncthreads();
   }
@@ -316,22 +374,20 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
 // window of each stream is its 5-slot MFCC ring in arrival order
 // (slot (count + d) % 5, oldest first); classify it if count >= 5, then push
 // the new frame's MFCC into the oldest slot (:74 after :71).
-template <int KS0, int T1, int T2, int T3, int T4>
+template <int KS0, int T1, int T2, int T3, int T4, int NC>
 __global__ __launch_bounds__(256) void stream_ffn_kernel(FfnDev net, const float* __restrict__ newrow,
                                                          float* __restrict__ ring,
                                                          int* __restrict__ count, int64_t n_streams,
                                                          int mfcc_n, uint8_t* __restrict__ labels) {
-  using TP = Topo<KS0, T1, T2, T3, T4>;
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int jw = lane & 15;
   const int in_dim = net.dims[0];
   float fa[TP::NA];
   float fb[TP::NB];
-#pragma unroll
-  for (int s = 0; s < TP::NA; ++s) fa[s] = net.frag[s * 64 + lane];
-#pragma unroll
-  for (int s = 0; s < TP::NB; ++s) fb[s] = net.frag[(TP::NA + s) * 64 + lane];
+  float fv[TP::NV + TP::NVB + 1];
+  load_frags<TP>(net.frag, lane, fa, fb, fv);
 
   const int64_t n_tiles = (n_streams + 15) / 16;
   const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -354,7 +410,7 @@ __global__ __launch_bounds__(256) void stream_ffn_kernel(FfnDev net, const float
       }
       x[k] = v;
     }
-    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4>(fa, fb, x);
+    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     if (valid) {
       if (g == 0) labels[s] = have ? (uint8_t)argmax_classes(z, net.n_classes) : (uint8_t)255;
       float* dst = rs + (c % 5) * mfcc_n;
@@ -383,13 +439,13 @@ __global__ __launch_bounds__(256) void features_kernel(const float* __restrict__
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-template <int KS0, int T1, int T2, int T3, int T4>
+template <int KS0, int T1, int T2, int T3, int T4, int NC = 4>
 static hipError_t launch_stream_topo(const FfnDev& net, const float* newrow, float* ring, int* count,
                                      int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st) {
   const int64_t n_tiles = (n_streams + 15) / 16;
   int64_t blocks = (n_tiles + 3) / 4;
   if (blocks > 2048) blocks = 2048;
-  hipLaunchKernelGGL((stream_ffn_kernel<KS0, T1, T2, T3, T4>), dim3((int)blocks), dim3(256), 0, st,
+  hipLaunchKernelGGL((stream_ffn_kernel<KS0, T1, T2, T3, T4, NC>), dim3((int)blocks), dim3(256), 0, st,
                      net, newrow, ring, count, n_streams, mfcc_n, labels);
   return hipGetLastError();
 }
@@ -405,7 +461,7 @@ static int ffn_num_cus() {
   return n;
 }
 
-template <int KS0, int T1, int T2, int T3, int T4>
+template <int KS0, int T1, int T2, int T3, int T4, int NC = 4>
 static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64_t n_rows,
                               int mfcc_n, int mode, uint8_t* labels, hipStream_t st) {
   const int64_t n_tiles = (n_rows + 15) / 16;
@@ -418,13 +474,13 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
     const int64_t cap = 2 * ffn_num_cus();
     if (chunks > cap) chunks = cap;
     if (mfcc_n == 13)
-      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, 13>), dim3((int)chunks), dim3(256), 0,
+      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, NC, 13>), dim3((int)chunks), dim3(256), 0,
                          st, net, in, n_rows, mfcc_n, mode, labels);
     else
-      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, 0>), dim3((int)chunks), dim3(256), 0,
+      hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, NC, 0>), dim3((int)chunks), dim3(256), 0,
                          st, net, in, n_rows, mfcc_n, mode, labels);
   } else
-    hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, kFromRows>), dim3((int)blocks), dim3(256), 0,
+    hipLaunchKernelGGL((ffn_kernel<KS0, T1, T2, T3, T4, NC, kFromRows>), dim3((int)blocks), dim3(256), 0,
                        st, net, in, n_rows, mfcc_n, mode, labels);
   return hipGetLastError();
 }
@@ -438,8 +494,11 @@ hipError_t launch_ffn(const FfnDev& net, int src, const float* in, int64_t n_row
   const int* t = net.tiles;
   if (net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1)
     return launch_topo<10, 4, 2, 1, 1>(net, src, in, n_rows, mfcc_n, mode, labels, st);
-  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1)
+  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1) {
+    if (net.n_classes <= 2)
+      return launch_topo<4, 4, 4, 1, 0, 2>(net, src, in, n_rows, mfcc_n, mode, labels, st);
     return launch_topo<4, 4, 4, 1, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
+  }
   switch (net.n_layers) {
     case 1: return launch_topo<16, 1, 0, 0, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
     case 2: return launch_topo<16, 4, 1, 0, 0>(net, src, in, n_rows, mfcc_n, mode, labels, st);
@@ -454,8 +513,11 @@ hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring
   const int* t = net.tiles;
   if (net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1)
     return launch_stream_topo<10, 4, 2, 1, 1>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
-  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1)
+  if (net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1) {
+    if (net.n_classes <= 2)
+      return launch_stream_topo<4, 4, 4, 1, 0, 2>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
     return launch_stream_topo<4, 4, 4, 1, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
+  }
   switch (net.n_layers) {
     case 1: return launch_stream_topo<16, 1, 0, 0, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
     case 2: return launch_stream_topo<16, 4, 1, 0, 0>(net, newrow, ring, count, n_streams, mfcc_n, labels, st);
