@@ -80,6 +80,15 @@ int vad_spec_f32(const vad_mfcc_plan* plan, const float* src, int64_t frame_stri
 int vad_mfcc_f32(const vad_mfcc_plan* plan, const float* src, int64_t frame_stride,
                  int32_t frame_len, int64_t n_frames, float* mfcc, void* stream);
 
+/* int16 PCM input: the same as vad_spec_f32 / vad_mfcc_f32 on the samples
+ * converted to fp32 (exact), i.e. the reference's int16 wav data followed by
+ * astype(float32) (vad.py:37, dataset/file_processing.py:26-35), at half the
+ * input bytes.  Frames are src + f*frame_stride (in samples). */
+int vad_spec_i16(const vad_mfcc_plan* plan, const int16_t* src, int64_t frame_stride,
+                 int32_t frame_len, int64_t n_frames, float* spec, void* stream);
+int vad_mfcc_i16(const vad_mfcc_plan* plan, const int16_t* src, int64_t frame_stride,
+                 int32_t frame_len, int64_t n_frames, float* mfcc, void* stream);
+
 /* get_mfcc_from_spec (mfcc.py:72-78) of n spectra spec[f*256 + k]. */
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* plan, const float* spec, int64_t n,
                            float* mfcc, void* stream);

@@ -138,6 +138,36 @@ def test_clip_mfcc_and_offline_features(torch_cuda, golden):
     assert rel.max() <= 10 * MFCC_TOL
 
 
+@pytest.mark.parametrize("nf", [26, 40])
+def test_int16_input_matches_fp32(torch_cuda, fb26, nf):
+    """int16 PCM input (vad.py:37 astype(float32)) == the fp32 path, bitwise:
+    the conversion is exact and the arithmetic after the load identical.
+    Covers the compiled-table kernel (400-sample frames, aligned pairs), the
+    unaligned-pair path (odd frame stride) and the spectrum entry."""
+    from vad_amd.plan import MfccPlan
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    x16 = np.clip(O.synth_clip(160 * 4000 + 241, 5), -32768, 32767).astype(np.int16)
+    x16[:2000] = rng.integers(-32768, 32767, 2000, dtype=np.int16)  # full range, incl. -32768
+    fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+    plan = MfccPlan(fb)
+    a16 = torch.from_numpy(x16).cuda()
+    a32 = a16.float()
+    m16 = plan.clip_mfcc(a16)
+    m32 = plan.clip_mfcc(a32)
+    assert torch.equal(m16, m32)
+    for stride, n in ((161, 500), (160, 4000)):
+        s16 = plan.spec(a16, frame_len=400, frame_stride=stride, n=n)
+        s32 = plan.spec(a32, frame_len=400, frame_stride=stride, n=n)
+        assert torch.equal(s16, s32)
+        q16 = plan.mfcc(a16, frame_len=400, frame_stride=stride, n=n)
+        q32 = plan.mfcc(a32, frame_len=400, frame_stride=stride, n=n)
+        assert torch.equal(q16, q32)
+    # and against the oracle on the int16 values
+    ref = O.mfcc_batch(x16[: 160 * 299 + 401].astype(np.float32), fb)
+    assert_mfcc_close(m16[:300].cpu().numpy(), ref)
+
+
 def test_framing_edge_lengths(torch_cuda, fb26):
     from vad_amd.pipeline import VadPipeline
     pipe = VadPipeline()

@@ -12,6 +12,7 @@ __global__ void bench(float* out, unsigned long long* cyc, int iters) {
   for (int i = 0; i < 32; ++i) s[i] = (float)threadIdx.x + i;
   const v2f m = (v2f){1.0001f, 0.9999f};
   const v2f c = (v2f){0.5f, 0.25f};
+  const float sg = __builtin_amdgcn_readfirstlane((int)threadIdx.x) * 0.5f;
   __syncthreads();
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < iters; ++it) {
@@ -26,6 +27,8 @@ __global__ void bench(float* out, unsigned long long* cyc, int iters) {
       if constexpr (KIND == 3) asm volatile("v_add_f32 %0, %0, %1" : "+v"(s[i]) : "v"(c.x));
       if constexpr (KIND == 4) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(s[i]) : "v"(m.x), "v"(c.x));
       if constexpr (KIND == 5) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a[i]) : "v"(m));
+      if constexpr (KIND == 6) asm volatile("v_fmac_f32_e32 %0, 0x3f812345, %1" : "+v"(s[i]) : "v"(c.x));
+      if constexpr (KIND == 7) asm volatile("v_fmac_f32_e32 %0, %1, %2" : "+v"(s[i]) : "s"(sg), "v"(c.x));
     }
   }
   unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -73,6 +76,8 @@ int main() {
     run<3>("v_add_f32", t);
     run<4>("v_fmac_f32", t);
     run<5>("v_pk_mul_f32", t);
+    run<6>("v_fmac literal", t);
+    run<7>("v_fmac sgpr", t);
   }
   return 0;
 }

@@ -13,6 +13,8 @@ from vad_amd.pipeline import VadPipeline  # noqa: E402
 pipe = VadPipeline()
 F = 1_000_000
 audio = synth_audio(160 * (F - 1) + 401, 1, torch.device("cuda"))
+if os.environ.get("VAD_STAMP_INT16"):
+    audio = audio.to(torch.int16)
 out = torch.zeros((F, 13), dtype=torch.float32, device="cuda")
 for _ in range(3):
     pipe.mfcc(audio, out=out)

@@ -35,6 +35,8 @@ SIGNATURES = {
     "vad_mfcc_plan_set_variant": (c_int, [c_vp, c_i32]),
     "vad_spec_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
     "vad_mfcc_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
+    "vad_spec_i16": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
+    "vad_mfcc_i16": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
     "vad_mfcc_from_spec_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "vad_ffn_plan_create": (c_int, [c_i32, c_vp, c_vp, c_vp, c_vp]),
     "vad_ffn_plan_destroy": (c_int, [c_vp]),

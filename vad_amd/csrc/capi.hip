@@ -170,6 +170,20 @@ int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
   return (int)launch_mfcc(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
+int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,
+                 float* spec, void* stream) {
+  int r = check_frames(p, src, stride, len, n, spec);
+  if (r || n == 0) return r;
+  return (int)launch_mfcc_i16(1, p->dev, 0, src, stride, len, n, spec, (hipStream_t)stream);
+}
+
+int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,
+                 float* mfcc, void* stream) {
+  int r = check_frames(p, src, stride, len, n, mfcc);
+  if (r || n == 0) return r;
+  return (int)launch_mfcc_i16(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
+}
+
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
                            void* stream) {
   int r = check_frames(p, spec, kBins, kBins, n, mfcc);

@@ -27,6 +27,8 @@
 //            finish their FFT first -- two barriers per tile.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "vad_common.h"
 #include "fft_pk.h"
 #include "mel_tables.h"
@@ -44,14 +46,36 @@ constexpr int kPStride = kBins + 4;  // floats per P row: 16-B aligned rows, con
 
 enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 
+// Sample loads by input type: fp32, or int16 PCM (the reference reads int16
+// audio and converts with astype(float32), vad.py:37 / file_processing.py:26-35;
+// the conversion is exact, so both inputs give identical spectra).
+template <typename TIN>
+struct Samples;
+template <>
+struct Samples<float> {
+  static constexpr int kPairAlign = 8;  // bytes for one aligned 2-sample load
+  __device__ static v2f pair(const float* p) { return *reinterpret_cast<const v2f*>(p); }
+  __device__ static float one(const float* p) { return *p; }
+};
+template <>
+struct Samples<int16_t> {
+  static constexpr int kPairAlign = 4;
+  __device__ static v2f pair(const int16_t* p) {
+    const int v = *reinterpret_cast<const int*>(p);
+    return (v2f){(float)(int16_t)(v & 0xffff), (float)(v >> 16)};
+  }
+  __device__ static float one(const int16_t* p) { return (float)*p; }
+};
+
 // Load z[16 n1 + n2] = (x[32 n1 + 2 n2], x[32 n1 + 2 n2 + 1]), n1 < NZ.
 // Branch-free and wait-free: every load is issued unconditionally from an
 // address clamped into the frame, so all NZ loads of a pass are in flight
 // at once; the zero padding (x[t] = 0 for t >= len) is applied later by
 // pad_stage_a, at first use.  LEN > 0 fixes the frame length at compile time
-// (400 for clips); VEC2 (8-byte aligned frames of even length) loads 8 B.
-template <int NZ, bool VEC2, int LEN>
-__device__ __forceinline__ void load_stage_a(const float* __restrict__ fr, int len_rt, int n2,
+// (400 for clips); VEC2 (pair-aligned frames of even length) loads a sample
+// pair per load.
+template <typename TIN, int NZ, bool VEC2, int LEN>
+__device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len_rt, int n2,
                                              v2f (&u)[NZ]) {
   const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
@@ -59,11 +83,11 @@ __device__ __forceinline__ void load_stage_a(const float* __restrict__ fr, int l
     const int t = 32 * n1 + 2 * n2;
     if constexpr (VEC2) {
       const int tc = t < len - 2 ? t : len - 2;
-      u[n1] = *reinterpret_cast<const v2f*>(fr + tc);
+      u[n1] = Samples<TIN>::pair(fr + tc);
     } else {
       const int t0 = t < len - 1 ? t : len - 1;
       const int t1 = t + 1 < len - 1 ? t + 1 : len - 1;
-      u[n1] = (v2f){fr[t0], fr[t1]};
+      u[n1] = (v2f){Samples<TIN>::one(fr + t0), Samples<TIN>::one(fr + t1)};
     }
   }
 }
@@ -364,9 +388,9 @@ constexpr size_t kScrBytes = (size_t)kGroups * kGroupScratch * sizeof(v2f);  // 
 constexpr size_t kLmBytes = (size_t)kLmFloats * sizeof(float);               // 17,408
 
 // DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
-template <int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
-    const MfccDev* __restrict__ plan, const float* __restrict__ src, int64_t frame_stride,
+    const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* P = reinterpret_cast<float*>(smem);                      // [64][260] power rows
@@ -391,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         const int lf = i / kBins, k = i - lf * kBins;
         const int64_t f = f0 + lf;
         // the taps carry the FFT path's 2^-20: undo it on true spectra (exact)
-        P[lf * kPStride + k] = (f < n_frames) ? src[f * kBins + k] * 0x1p20f : 0.f;
+        P[lf * kPStride + k] = (f < n_frames) ? (float)src[f * kBins + k] * 0x1p20f : 0.f;
       }
       __syncthreads();  // P complete; the previous tile's phase 2b is done
       phase2a<SPEC>(plan, P, lm, wave, lane);
@@ -409,7 +433,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     auto load_pass = [&](int64_t t, int pass, v2f (&buf)[NZ]) {
       int64_t f = t * kTile + pass * kGroups + grp;
       f = f < flast ? f : flast;
-      load_stage_a<NZ, VEC2, LEN>(src + f * frame_stride, len, j, buf);
+      load_stage_a<TIN, NZ, VEC2, LEN>(src + f * frame_stride, len, j, buf);
     };
     int64_t tile = blockIdx.x;
     load_pass(tile, 0, bufA);
@@ -520,8 +544,8 @@ static int num_cus() {
   return n;
 }
 
-template <int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0>
-static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride, int len,
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0>
+static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
   const int cap = num_cus();  // persistent: one 512-thread workgroup per CU (LDS-bound)
@@ -529,52 +553,60 @@ static hipError_t launch_t(const MfccDev* plan, const float* src, int64_t stride
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC, DIAG>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mfcc_kernel<MODE, NZ, VEC2, LEN, SPEC, DIAG>), dim3(grid), dim3(kThreads), smem, st, plan,
-                     src, stride, len, n, out);
+  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG>), dim3(grid), dim3(kThreads),
+                     smem, st, plan, src, stride, len, n, out);
   return hipGetLastError();
 }
 
-template <int MODE>
-static hipError_t launch_m(const MfccDev* plan, int spec, const float* src, int64_t stride, int len,
+template <typename TIN, int MODE>
+static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int used = len < kFftN ? len : kFftN;
-  const bool vec2 = ((reinterpret_cast<uintptr_t>(src) & 7) == 0) && ((stride & 1) == 0) &&
-                    ((used & 1) == 0);
+  const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
+                    ((stride & 1) == 0) && ((used & 1) == 0);
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
-      if (diag == 5) return launch_t<MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 6) return launch_t<MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
-      return launch_t<MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
+      if (diag == 5) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 6) return launch_t<TIN, MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
+      return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2)
-      return launch_t<MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
-    return launch_t<MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
+      return launch_t<TIN, MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
+    return launch_t<TIN, MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
   }
   if (used <= 32 * 13) {
-    return vec2 ? launch_t<MODE, 13, true>(plan, src, stride, len, n, out, st)
-                : launch_t<MODE, 13, false>(plan, src, stride, len, n, out, st);
+    return vec2 ? launch_t<TIN, MODE, 13, true>(plan, src, stride, len, n, out, st)
+                : launch_t<TIN, MODE, 13, false>(plan, src, stride, len, n, out, st);
   }
-  return vec2 ? launch_t<MODE, 16, true>(plan, src, stride, len, n, out, st)
-              : launch_t<MODE, 16, false>(plan, src, stride, len, n, out, st);
+  return vec2 ? launch_t<TIN, MODE, 16, true>(plan, src, stride, len, n, out, st)
+              : launch_t<TIN, MODE, 16, false>(plan, src, stride, len, n, out, st);
 }
 
 hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
                        int len, int64_t n, float* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   switch (mode) {
-    case kAudioToMfcc: return launch_m<kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
-    case kAudioToSpec: return launch_m<kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
+    case kAudioToMfcc: return launch_m<float, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
+    case kAudioToSpec: return launch_m<float, kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
     default:
-      if (spec == 1) return launch_t<kSpecToMfcc, 13, false, 0, 1>(plan, src, 0, 0, n, out, st);
-      if (spec == 2) return launch_t<kSpecToMfcc, 13, false, 0, 2>(plan, src, 0, 0, n, out, st);
-      return launch_t<kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
+      if (spec == 1) return launch_t<float, kSpecToMfcc, 13, false, 0, 1>(plan, src, 0, 0, n, out, st);
+      if (spec == 2) return launch_t<float, kSpecToMfcc, 13, false, 0, 2>(plan, src, 0, 0, n, out, st);
+      return launch_t<float, kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
   }
+}
+
+hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_t* src,
+                           int64_t stride, int len, int64_t n, float* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (mode == kAudioToSpec) return launch_m<int16_t, kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
+  return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
 }
 
 }  // namespace vad

@@ -80,7 +80,10 @@ class MfccPlan:
     # -- frame sources ------------------------------------------------------
     @staticmethod
     def _frames_args(src, frame_len, frame_stride, n):
-        _require_cuda_tensor(src, "src")
+        if isinstance(src, torch.Tensor) and src.dtype == torch.int16:
+            _require_cuda_tensor(src, "src", torch.int16)
+        else:
+            _require_cuda_tensor(src, "src")
         if src.dim() == 2 and frame_len is None:
             n, frame_len = src.shape
             frame_stride = frame_len
@@ -91,26 +94,31 @@ class MfccPlan:
         return int(frame_len), int(frame_stride), int(n)
 
     def spec(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
-        """get_spec_mag (mfcc.py:59-61) of every frame -> (n, 256) fp32."""
+        """get_spec_mag (mfcc.py:59-61) of every frame -> (n, 256) fp32 (src fp32 or int16)."""
         frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
         if out is None:
             out = torch.empty((n, self.fft_n // 2), dtype=torch.float32, device=src.device)
-        check(lib().vad_spec_f32(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
-                                 stream_ptr(stream)), "vad_spec_f32")
+        fn = "vad_spec_i16" if src.dtype == torch.int16 else "vad_spec_f32"
+        check(getattr(lib(), fn)(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
+                                 stream_ptr(stream)), fn)
         return out
 
     def mfcc(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
-        """get_mfcc (mfcc.py:67-69) of every frame -> (n, mfcc_n) fp32."""
+        """get_mfcc (mfcc.py:67-69) of every frame -> (n, mfcc_n) fp32 (src fp32 or int16)."""
         frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
         if out is None:
             out = torch.empty((n, self.mfcc_n), dtype=torch.float32, device=src.device)
-        check(lib().vad_mfcc_f32(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
-                                 stream_ptr(stream)), "vad_mfcc_f32")
+        fn = "vad_mfcc_i16" if src.dtype == torch.int16 else "vad_mfcc_f32"
+        check(getattr(lib(), fn)(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
+                                 stream_ptr(stream)), fn)
         return out
 
     def clip_mfcc(self, audio, frame_size=400, hop=160, out=None, stream=None):
-        """MFCC of every frame split_into_frames takes from a clip (file_processing.py:80-103)."""
-        _require_cuda_tensor(audio, "audio")
+        """MFCC of every frame split_into_frames takes from a clip (file_processing.py:80-103).
+
+        `audio` is fp32, or int16 PCM (converted exactly on load, like the
+        reference's astype(float32) of its int16 wav data, vad.py:37)."""
+        _require_cuda_tensor(audio, "audio", audio.dtype if audio.dtype == torch.int16 else torch.float32)
         f = n_frames(audio.numel(), frame_size, hop)
         return self.mfcc(audio, frame_len=frame_size, frame_stride=hop, n=f, out=out, stream=stream)
 
