@@ -387,6 +387,19 @@ constexpr size_t kPBytes = (size_t)kTile * kPStride * sizeof(float);          //
 constexpr size_t kScrBytes = (size_t)kGroups * kGroupScratch * sizeof(v2f);  // 73,728
 constexpr size_t kLmBytes = (size_t)kLmFloats * sizeof(float);               // 17,408
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// operations (lgkmcnt) but not for its vector-memory ones (__syncthreads'
+// release fence would drain vmcnt, i.e. wait for the next tile's sample
+// loads at every barrier and cut the prefetch distance to a fraction of a
+// tile); the empty asm statements keep the compiler from moving memory
+// accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // vmcnt 63, expcnt 7, lgkmcnt 0
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
@@ -431,13 +444,23 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     v2f bufA[NZ], bufB[NZ];
     const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
     auto load_pass = [&](int64_t t, int pass, v2f (&buf)[NZ]) {
+      if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
       int64_t f = t * kTile + pass * kGroups + grp;
       f = f < flast ? f : flast;
       load_stage_a<TIN, NZ, VEC2, LEN>(src + f * frame_stride, len, j, buf);
     };
-    int64_t tile = blockIdx.x;
+    // each workgroup owns a contiguous run of tiles: consecutive tiles are
+    // adjacent in memory (shared halo in this XCD's L2, page-local loads)
+    const int64_t per = (n_tiles + gridDim.x - 1) / gridDim.x;
+    const int64_t t_end = ((int64_t)blockIdx.x + 1) * per < n_tiles ? ((int64_t)blockIdx.x + 1) * per : n_tiles;
+    int64_t tile = (int64_t)blockIdx.x * per;
+    // issue order = the steady state's (pass 0 then pass 1): the waitcnt
+    // pass merges the prologue into the loop header, and an interleaved
+    // prologue would make the first stage A wait for every load in flight
     load_pass(tile, 0, bufA);
+    __builtin_amdgcn_sched_barrier(0);
     load_pass(tile, 1, bufB);
+    __builtin_amdgcn_sched_barrier(0);
     unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
     int it = 0;
     (void)stamps;
@@ -447,7 +470,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // ones; pass 1's stage A runs while pass 0's transpose reads are in
     // flight.  sched_barriers pin that order (the scheduler would otherwise
     // hoist the loads or sink the reads).
-    for (; tile < n_tiles; tile += gridDim.x, ++it) {
+    for (; tile < t_end; ++tile, ++it) {
       const int64_t f0 = tile * kTile;
       const int64_t fa = f0 + grp, fb = f0 + kGroups + grp;
       float* prow_a;
@@ -469,7 +492,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         stage_a<NZ, LEN>(bufA, len, L, j, u);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
-        load_pass(tile + gridDim.x, 0, bufA);
+        load_pass(tile + 1, 0, bufA);
         __builtin_amdgcn_sched_barrier(0);
         store_a(u, gscr, j);
         read_b(L, gscr, col);
@@ -479,7 +502,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           VAD_STAMP(2);
           stage_a<NZ, LEN>(bufB, len, L, j, u);
           __builtin_amdgcn_sched_barrier(0);
-          load_pass(tile + gridDim.x, 1, bufB);
+          load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
           VAD_STAMP(3);
           if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
@@ -490,7 +513,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           __builtin_amdgcn_sched_barrier(0);
           stage_a<NZ, LEN>(bufB, len, L, j, u);
           __builtin_amdgcn_sched_barrier(0);
-          load_pass(tile + gridDim.x, 1, bufB);
+          load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
         }
         VAD_STAMP(4);
@@ -508,11 +531,11 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         if (prev_f0 >= 0 && wave < kDctGroups)
           phase2b<SPEC, DIAG < 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
         VAD_STAMP(7);
-        __syncthreads();  // P complete; log-mel rows consumed
+        lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
         if (work) phase2a<SPEC>(plan, P, lm, wave, lane);
         VAD_STAMP(9);
-        __syncthreads();  // log-mel rows complete; P and the FFT scratch free
+        lds_barrier();  // log-mel rows complete; P and the FFT scratch free
         VAD_STAMP(10);
         prev_f0 = f0;
         if constexpr (DIAG >= 5) {
@@ -575,6 +598,7 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
       if (diag == 5) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
       if (diag == 6) return launch_t<TIN, MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
+      if (diag == 7) return launch_t<TIN, MODE, 13, true, 400, 1, 7>(plan, src, stride, len, n, out, st);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2)
