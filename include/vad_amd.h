@@ -142,6 +142,34 @@ int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float
                  uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Decision-tree plan: the classifier vad.py deploys
+ * (learning/decision_classifier_trainer.py:26-35: sklearn
+ * DecisionTreeClassifier, predict through sklearn_analyser.py:71) as a flat
+ * node table, e.g. from an sklearn tree_: feature[i] (< 0 for a leaf),
+ * threshold[i] (float64), left[i] / right[i] (children_left / _right),
+ * leaf_class[i] = argmax of the leaf's value row (class index), and nan_left[i]
+ * (missing_go_to_left, sklearn >= 1.3; NULL: NaN goes right).  Traversal is
+ * sklearn's: left iff float32(x[feature]) <= threshold (compared in double).
+ * Returned labels are class indices (uint8); the caller maps them through
+ * classes_.  Constraints: 1 <= n_nodes <= 2^24, feature < n_features <= 64.
+ * ------------------------------------------------------------------------- */
+typedef struct vad_tree_plan vad_tree_plan;
+
+int vad_tree_plan_create(int32_t n_nodes, const int32_t* feature, const double* threshold,
+                         const int32_t* left, const int32_t* right, const int32_t* leaf_class,
+                         const uint8_t* nan_left, int32_t n_features, vad_tree_plan** out);
+int vad_tree_plan_destroy(vad_tree_plan* plan);
+
+/* labels[i] of caller-built feature rows x[i*n_features + f] (fp32). */
+int vad_tree_predict(const vad_tree_plan* tree, const float* x, int64_t n, uint8_t* labels,
+                     void* stream);
+
+/* Labels of every window of an MFCC sequence (features as vad_features_f32,
+ * mode VAD_FEAT_ANALYSER or VAD_FEAT_OFFLINE), labels[i], i < n_frames-5. */
+int vad_features_tree(const vad_tree_plan* tree, const float* mfcc, int64_t n_frames,
+                      int32_t mfcc_n, int32_t mode, uint8_t* labels, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Streaming: S independent analyser streams advanced by one frame each
  * (SKLearnAnalyzer.feed_frame, sklearn_analyser.py:46-82, for S streams at
  * once).  State lives in device buffers the caller allocates with the sizes

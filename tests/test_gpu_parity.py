@@ -424,3 +424,81 @@ def test_compiled_tables_match_runtime_path(torch_cuda, golden, nf):
     assert_mfcc_close(m_gen, ref)
     # a non-reference bank stays on the runtime path
     assert MfccPlan(O.get_mel_filterbanks(100, 4000, 512, 32, 16000)).variant == 0
+
+
+# ---------------------------------------------------------------------------
+# decision tree (decision_classifier_trainer.py:26-35, the classifier vad.py
+# deploys) -- sklearn's traversal on the GPU node table
+# ---------------------------------------------------------------------------
+def _tree(golden):
+    from vad_amd.tree import TreeClassifier
+    g = golden("tree")
+    return g, TreeClassifier(g["feature"], g["threshold"], g["left"], g["right"], g["leaf"],
+                             g["nan_left"], g["classes"], int(g["n_features"]))
+
+
+def test_tree_predict_matches_sklearn(torch_cuda, golden):
+    g, t = _tree(golden)
+    assert np.array_equal(t.predict(g["x_test"]), g["y_test"])
+
+
+def test_tree_window_labels_on_clip(torch_cuda, golden):
+    """Fused window features + tree walk == the oracle walk over the GPU's own
+    fp32 features (so the comparison is exact), analyser and offline modes;
+    plus VadPipeline(labels) with the tree."""
+    from vad_amd import _lib
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.plan import window_features
+    g, t = _tree(golden)
+    tree = {k: g[k] for k in ("feature", "threshold", "left", "right", "leaf", "nan_left",
+                              "classes")} | {"n_features": int(g["n_features"])}
+    clip = O.synth_clip(O.samples_for_frames(3000), 41)
+    clip[160 * 1000:160 * 1100] = 0.0  # digital silence: NaN features
+    pipe = VadPipeline(ffn=t)
+    a = torch_cuda.from_numpy(clip).cuda()
+    m = pipe.mfcc(a)
+    for mode in (_lib.FEAT_ANALYSER, _lib.FEAT_OFFLINE):
+        feats = window_features(m, mode).cpu().numpy()
+        ref = O.tree_predict(tree, feats)
+        got = g["classes"][t.window_labels(m, mode).cpu().numpy()]
+        assert np.array_equal(got, ref)
+    assert np.isnan(window_features(m, _lib.FEAT_ANALYSER).cpu().numpy()).any()
+    lab = pipe.labels(a).cpu().numpy()
+    assert np.array_equal(g["classes"][lab], O.tree_predict(tree, window_features(m).cpu().numpy()))
+
+
+class _HostTree:
+    """The same sklearn tree kept on the host (the reference's call path)."""
+
+    def __init__(self, clf):
+        self.clf = clf
+
+    def predict(self, x):
+        return self.clf.predict(x)
+
+
+def test_analyser_with_pickled_sklearn_tree(torch_cuda, golden, tmp_path):
+    """SKLearnAnalyzer(pickled DecisionTreeClassifier): the tree moves to the
+    GPU and the feed_frame trace equals the host-sklearn call path."""
+    from sklearn.tree import DecisionTreeClassifier
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    from vad_amd.tree import TreeClassifier
+    ga = golden("analyser")
+    gt = golden("tree")
+    clf = DecisionTreeClassifier(min_samples_split=22, max_depth=25, min_samples_leaf=20,
+                                 random_state=0).fit(np.nan_to_num(gt["x_test"]), gt["y_test"])
+    p1 = tmp_path / "tree.cls"
+    with open(p1, "wb") as f:
+        pickle.dump(clf, f)
+    p2 = tmp_path / "host.cls"
+    with open(p2, "wb") as f:
+        pickle.dump(_HostTree(clf), f)
+    an_gpu = SKLearnAnalyzer(str(p1))
+    assert isinstance(an_gpu.classifier, TreeClassifier)
+    an_host = SKLearnAnalyzer(str(p2))
+    for an in (an_gpu, an_host):
+        an.load_init_inactive_frames(list(ga["noise"]))
+    stream = list(ga["stream"])
+    for fr in stream:
+        r1, r2 = an_gpu.feed_frame(fr), an_host.feed_frame(fr)
+        assert (r1 is None and r2 is None) or (r1 is r2)

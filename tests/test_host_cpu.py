@@ -99,3 +99,17 @@ def test_ffn_layers_roundtrip(tmp_path):
         np.testing.assert_array_equal(b, b2)
     c = FFNClassifier.load(str(p))
     assert c.in_dim == 39
+
+
+def test_tree_table_roundtrip(tmp_path, golden):
+    """TreeClassifier keeps the node table bit for bit through .npz (no pickle)."""
+    from vad_amd.tree import TreeClassifier
+    g = golden("tree")
+    t = TreeClassifier(g["feature"], g["threshold"], g["left"], g["right"], g["leaf"],
+                       g["nan_left"], g["classes"], int(g["n_features"]))
+    p = tmp_path / "tree.npz"
+    t.save(p)
+    u = TreeClassifier.load(p)
+    for k in ("feature", "threshold", "left", "right", "leaf", "nan_left", "classes_"):
+        assert np.array_equal(getattr(t, k), getattr(u, k))
+    assert u.n_features == t.n_features == 39

@@ -159,3 +159,35 @@ def test_fast_analyser_features_equal_loop(golden):
     np.testing.assert_array_equal(np.isnan(a), np.isnan(b))
     ok = ~np.isnan(a)
     assert np.allclose(a[ok], b[ok], rtol=1e-12, atol=1e-12)
+
+
+# ---------------------------------------------------------------------------
+# decision tree (decision_classifier_trainer.py:26-35)
+# ---------------------------------------------------------------------------
+def _tree_from_fixture(g):
+    return {k: g[k] for k in ("feature", "threshold", "left", "right", "leaf", "nan_left",
+                              "classes")} | {"n_features": int(g["n_features"])}
+
+
+def test_tree_oracle_matches_sklearn_fixture(golden):
+    """The restated traversal reproduces the predictions sklearn recorded
+    (fixture made by tests/golden/gen_tree.py, incl. NaN feature rows)."""
+    g = golden("tree")
+    pred = O.tree_predict(_tree_from_fixture(g), g["x_test"])
+    assert np.array_equal(pred, g["y_test"])
+    assert np.isnan(g["x_test"]).any()
+
+
+def test_tree_oracle_matches_live_sklearn():
+    """Pin the restatement against the installed sklearn on fresh data: ties
+    at thresholds (float32 grid), NaNs, three classes."""
+    from sklearn.tree import DecisionTreeClassifier
+    rng = np.random.default_rng(3)
+    X = np.round(rng.standard_normal((3000, 7)) * 4).astype(np.float32) / 4  # many exact ties
+    y = (X[:, 0] + X[:, 1] > 0).astype(int) + (X[:, 2] > 1).astype(int)
+    X[rng.random(X.shape) < 0.02] = np.nan
+    clf = DecisionTreeClassifier(min_samples_split=22, max_depth=25, min_samples_leaf=20,
+                                 random_state=1).fit(X, y)
+    Xt = np.round(rng.standard_normal((2000, 7)) * 4).astype(np.float32) / 4
+    Xt[rng.random(Xt.shape) < 0.05] = np.nan
+    assert np.array_equal(O.tree_predict(O.tree_arrays(clf), Xt), clf.predict(Xt))

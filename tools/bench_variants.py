@@ -76,6 +76,23 @@ def main():
         t = timed(step, max(10, a.reps // 2))
         res[f"C3_mfcc_ffn_{name}"] = {"frames_per_s": F / t, "us": t * 1e6}
 
+    # MFCC + decision tree (the classifier vad.py deploys), fixture tree
+    from vad_amd.tree import TreeClassifier
+    gt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests",
+                      "golden", "tree.npz")
+    with __import__("numpy").load(gt, allow_pickle=False) as g:
+        tree = TreeClassifier(g["feature"], g["threshold"], g["left"], g["right"], g["leaf"],
+                              g["nan_left"], g["classes"], int(g["n_features"]))
+    lab = torch.empty((F - 5,), dtype=torch.uint8, device=dev)
+
+    def step_tree():
+        m = pipe.mfcc(x, out=out)
+        tree.window_labels(m, out=lab)
+    t = timed(step_tree, max(10, a.reps // 2))
+    tt = timed(lambda: tree.window_labels(out, out=lab), max(10, a.reps // 2))
+    res["C3_mfcc_tree"] = {"frames_per_s": F / t, "us": t * 1e6, "tree_kernel_us": tt * 1e6,
+                           "nodes": int(len(tree.feature))}
+
     # C5: 512 streams, one 10 ms hop per step, replayed hipGraph
     S = 512
     clf = ffn_mod.FFNClassifier(ffn_mod.random_layers(ffn_mod.TOPOLOGY_BL13, seed=3))

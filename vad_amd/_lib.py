@@ -43,6 +43,10 @@ SIGNATURES = {
     "vad_features_f32": (c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "vad_features_ffn": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "vad_ffn_predict": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "vad_tree_plan_create": (c_int, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
+    "vad_tree_plan_destroy": (c_int, [c_vp]),
+    "vad_tree_predict": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "vad_features_tree": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "vad_mfcc_ffn_workspace_bytes": (c_sz, [c_vp, c_i64, c_i32, c_i32]),
     "vad_mfcc_ffn": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_sz,
                              c_vp]),

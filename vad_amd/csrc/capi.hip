@@ -280,6 +280,76 @@ int vad_ffn_plan_destroy(vad_ffn_plan* p) {
   return VAD_OK;
 }
 
+struct vad_tree_plan {
+  TreeNode* nodes_dev;
+  int n_nodes;
+  int n_features;
+};
+
+int vad_tree_plan_create(int32_t n_nodes, const int32_t* feature, const double* threshold,
+                         const int32_t* left, const int32_t* right, const int32_t* leaf_class,
+                         const uint8_t* nan_left, int32_t n_features, vad_tree_plan** out) {
+  if (!feature || !threshold || !left || !right || !leaf_class || !out || n_nodes <= 0 ||
+      n_features <= 0)
+    return VAD_EINVAL;
+  if (n_nodes > (1 << 24) || n_features > 3 * VAD_MAX_MFCC + 16) return VAD_EUNSUPPORTED;
+  std::vector<TreeNode> h((size_t)n_nodes);
+  for (int i = 0; i < n_nodes; ++i) {
+    TreeNode& nd = h[i];
+    nd.feature = feature[i] >= 0 ? feature[i] : -1;
+    nd.threshold = threshold[i];
+    nd.left = left[i];
+    nd.right = right[i];
+    nd.leaf = (short)(leaf_class[i] < 0 || leaf_class[i] > 255 ? -1 : leaf_class[i]);
+    nd.nan_left = (short)(nan_left ? (nan_left[i] != 0) : 0);
+    if (nd.feature >= 0) {  // internal: children in range, feature in the row
+      if (nd.feature >= n_features || nd.left <= 0 || nd.left >= n_nodes || nd.right <= 0 ||
+          nd.right >= n_nodes)
+        return VAD_EINVAL;
+    } else if (nd.leaf < 0) {
+      return VAD_EINVAL;
+    }
+  }
+  vad_tree_plan* p = (vad_tree_plan*)calloc(1, sizeof(vad_tree_plan));
+  if (!p) return VAD_ENOMEM;
+  hipError_t e = hipMalloc((void**)&p->nodes_dev, h.size() * sizeof(TreeNode));
+  if (e != hipSuccess) { free(p); return (int)e; }
+  e = hipMemcpy(p->nodes_dev, h.data(), h.size() * sizeof(TreeNode), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->nodes_dev); free(p); return (int)e; }
+  p->n_nodes = n_nodes;
+  p->n_features = n_features;
+  *out = p;
+  return VAD_OK;
+}
+
+int vad_tree_plan_destroy(vad_tree_plan* p) {
+  if (!p) return VAD_OK;
+  (void)hipFree(p->nodes_dev);
+  free(p);
+  return VAD_OK;
+}
+
+int vad_tree_predict(const vad_tree_plan* t, const float* x, int64_t n, uint8_t* labels,
+                     void* stream) {
+  if (!t || n < 0) return VAD_EINVAL;
+  if (n == 0) return VAD_OK;
+  if (!x || !labels) return VAD_EINVAL;
+  return (int)launch_tree_rows(t->nodes_dev, t->n_nodes, x, n, t->n_features, labels,
+                               (hipStream_t)stream);
+}
+
+int vad_features_tree(const vad_tree_plan* t, const float* mfcc, int64_t n_frames, int32_t mfcc_n,
+                      int32_t mode, uint8_t* labels, void* stream) {
+  if (!t || n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  if (t->n_features > 3 * mfcc_n) return VAD_EINVAL;
+  const int64_t rows = n_frames > 5 ? n_frames - 5 : 0;
+  if (rows == 0) return VAD_OK;
+  if (!mfcc || !labels) return VAD_EINVAL;
+  return (int)launch_tree_windows(t->nodes_dev, t->n_nodes, mfcc, rows, mfcc_n, mode, labels,
+                                  (hipStream_t)stream);
+}
+
 int vad_features_f32(const float* mfcc, int64_t n_frames, int32_t mfcc_n, int32_t mode,
                      float* features, void* stream) {
   if (n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))

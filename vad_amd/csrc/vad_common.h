@@ -46,6 +46,18 @@ struct FfnDev {
   const float* frag;              // [slot][64] per-lane fragments: A operands, then biases
 };
 
+// Decision-tree node (tree_kernel.hip): internal if feature >= 0 (go left
+// iff x[feature] <= threshold, or x[feature] is NaN and nan_left), else a
+// leaf of class index `leaf`.
+struct TreeNode {
+  int feature;
+  int left;
+  int right;
+  short leaf;
+  short nan_left;  // a NaN feature goes left (sklearn missing_go_to_left)
+  double threshold;
+};
+
 // Launchers (defined in the .hip translation units).
 size_t mfcc_smem_bytes();
 hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
@@ -58,6 +70,10 @@ hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring
                              int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st);
 hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
                            hipStream_t st);
+hipError_t launch_tree_rows(const TreeNode* nodes, int n_nodes, const float* x, int64_t n, int dim,
+                            uint8_t* labels, hipStream_t st);
+hipError_t launch_tree_windows(const TreeNode* nodes, int n_nodes, const float* mfcc, int64_t n_rows,
+                               int mfcc_n, int mode, uint8_t* labels, hipStream_t st);
 
 // NaN-keeping ReLU (numpy / Keras keep NaN; fmaxf would drop it).
 __device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }

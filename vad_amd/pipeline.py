@@ -39,9 +39,14 @@ class VadPipeline:
     "offline" (file_processing.py:40-70 features)."""
 
     def __init__(self, ffn=None, cfg: MfccConfig = MfccConfig(), mode="analyser"):
+        """ffn: an FFNClassifier (or its layers), or a TreeClassifier / fitted
+        sklearn DecisionTreeClassifier (the classifier vad.py deploys)."""
+        from .tree import TreeClassifier
         self.cfg = cfg
         self.plan = MfccPlan.from_config(cfg)
-        if ffn is not None and not isinstance(ffn, FFNClassifier):
+        if ffn is not None and TreeClassifier.looks_like_sklearn_tree(ffn):
+            ffn = TreeClassifier.from_sklearn(ffn)
+        if ffn is not None and not isinstance(ffn, (FFNClassifier, TreeClassifier)):
             ffn = FFNClassifier(ffn)
         self.ffn = ffn
         self.mode = _lib.FEAT_ANALYSER if mode == "analyser" else _lib.FEAT_OFFLINE
@@ -74,6 +79,9 @@ class VadPipeline:
         rows = max(f - 5, 0)
         if out is None:
             out = torch.empty((rows,), dtype=torch.uint8, device=audio.device)
+        if not isinstance(self.ffn, FFNClassifier):  # decision tree: MFCC, then windows
+            return self.ffn.window_labels(self.mfcc(audio, stream=stream), self.mode, out=out,
+                                          stream=stream)
         need = self.workspace_bytes(audio.numel())
         if need and (self._ws is None or self._ws.numel() < need):
             self._ws = torch.empty((need,), dtype=torch.uint8, device=audio.device)

@@ -15,9 +15,11 @@ is unused, :122-123), so only its bookkeeping is kept.
 
 Classifier: an ``.npz`` of FFN weights (or a pickled ``FFNClassifier``) runs
 the fused GPU step -- MFCC of the new frame, window features and the MFMA FFN
-in two kernel launches, state in device memory.  Any other pickled object
-with ``.predict`` is called with the (1, 39) float64 feature row computed on
-the GPU, exactly as the reference calls it.
+in two kernel launches, state in device memory.  A decision tree (an ``.npz``
+node table, or a pickled sklearn ``DecisionTreeClassifier`` -- the classifier
+vad.py deploys) is walked on the GPU over the GPU feature row.  Any other
+pickled object with ``.predict`` is called with the (1, 39) float64 feature
+row computed on the GPU, exactly as the reference calls it.
 """
 from __future__ import annotations
 
@@ -33,6 +35,7 @@ from .config import FRAMES_BUFFER_SIZE, NOISE_BUFFER_SIZE, PROCESSING_FRAME_INDE
 from .ffn import FFNClassifier
 from .mfcc import get_mel_filterbanks
 from .plan import MfccPlan, window_features
+from .tree import TreeClassifier
 
 logger = logging.getLogger(__name__)
 
@@ -58,10 +61,17 @@ class SKLearnAnalyzer(Analyser):
         self.noise_buffer = []
 
         if str(fname).endswith(".npz"):
-            self.classifier = FFNClassifier.load(fname)
+            with np.load(fname, allow_pickle=False) as z:
+                is_tree = "threshold" in z.files
+            self.classifier = TreeClassifier.load(fname) if is_tree else FFNClassifier.load(fname)
         else:
+            # the reference unpickles its classifier file (:34-35); a fitted
+            # sklearn decision tree (decision_classifier_trainer.py) moves to
+            # the GPU node table, anything else keeps its own predict
             with open(fname, "rb") as f:
                 self.classifier = pickle.load(f)
+            if TreeClassifier.looks_like_sklearn_tree(self.classifier):
+                self.classifier = TreeClassifier.from_sklearn(self.classifier)
 
         self._plan = MfccPlan(self.filterbank, mfcc_num, fft_n)
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -138,8 +148,11 @@ class SKLearnAnalyzer(Analyser):
         mf = self._plan.mfcc(x, frame_len=n, frame_stride=n, n=1, out=self._scratch)
         if len(self.frames_buffer) == self.FRAMES_BUFFER_SIZE:
             feats = window_features(self._window, _lib.FEAT_ANALYSER)  # (1, 39)
-            row = feats.cpu().numpy().astype(np.float64).reshape(1, -1)
-            cls = self.classifier.predict(row)
+            if isinstance(self.classifier, TreeClassifier):  # GPU node table
+                cls = self.classifier.classes_[int(self.classifier.predict_device(feats).item())]
+            else:
+                row = feats.cpu().numpy().astype(np.float64).reshape(1, -1)
+                cls = self.classifier.predict(row)
             label = 1 if cls == 1 else 0 if cls == 0 else 2
         w = self._window
         w[:self.FRAMES_BUFFER_SIZE - 1].copy_(w[1:self.FRAMES_BUFFER_SIZE].clone())
