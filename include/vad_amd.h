@@ -170,6 +170,28 @@ int vad_features_tree(const vad_tree_plan* tree, const float* mfcc, int64_t n_fr
                       int32_t mfcc_n, int32_t mode, uint8_t* labels, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Offline dataset export (dataset_creator.py:58-66 -> file_processing.py,
+ * dataset/utils.py).
+ * ------------------------------------------------------------------------- */
+
+/* scale_features (dataset/utils.py:5-34) of feature rows
+ * rows[i*3*mfcc_n + t*mfcc_n + c] (t: mfcc / delta1 / delta2, the OFFLINE
+ * layout), in place on the device: one global mean and population std per
+ * group t over all rows, x = (x - mean_t) / std_t; statistics in fp64.
+ * `workspace` (device, >= vad_scale_workspace_bytes()) ends with the six
+ * doubles mean[3], std[3]. */
+size_t vad_scale_workspace_bytes(void);
+int vad_scale_features(float* rows, int64_t n_rows, int32_t mfcc_n, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* CSV text of host feature rows as write_features writes them
+ * (file_processing.py:126-146: features, then the label; values printed like
+ * numpy float32, rows ending in "\r\n").  Returns the bytes written, or
+ * -(bytes needed) when buf is NULL or too small. */
+int64_t vad_format_csv_rows(const float* rows, int64_t n_rows, int32_t n_cols, double label,
+                            char* buf, int64_t buf_size);
+
+/* ---------------------------------------------------------------------------
  * Streaming: S independent analyser streams advanced by one frame each
  * (SKLearnAnalyzer.feed_frame, sklearn_analyser.py:46-82, for S streams at
  * once).  State lives in device buffers the caller allocates with the sizes

@@ -350,6 +350,23 @@ int vad_features_tree(const vad_tree_plan* t, const float* mfcc, int64_t n_frame
                                   (hipStream_t)stream);
 }
 
+size_t vad_scale_workspace_bytes(void) { return scale_workspace_bytes(); }
+
+int vad_scale_features(float* rows, int64_t n_rows, int32_t mfcc_n, void* workspace,
+                       size_t workspace_bytes, void* stream) {
+  if (n_rows < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC) return VAD_EINVAL;
+  if (n_rows == 0) return VAD_OK;
+  if (!rows || !workspace || workspace_bytes < scale_workspace_bytes()) return VAD_EINVAL;
+  return (int)launch_scale_features(rows, n_rows, mfcc_n, (double*)workspace, (hipStream_t)stream);
+}
+
+int64_t vad_format_csv_rows(const float* rows, int64_t n_rows, int32_t n_cols, double label,
+                            char* buf, int64_t buf_size) {
+  if (n_rows < 0 || n_cols <= 0 || (n_rows > 0 && !rows)) return VAD_EINVAL;
+  if (n_rows == 0) return 0;
+  return format_csv_rows(rows, n_rows, n_cols, label, buf, buf_size);
+}
+
 int vad_features_f32(const float* mfcc, int64_t n_frames, int32_t mfcc_n, int32_t mode,
                      float* features, void* stream) {
   if (n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))

@@ -19,17 +19,10 @@ from .plan import MfccPlan, n_frames, window_features
 
 
 def split_into_frames(data, frame_size, step, transcription_path=None, frame_rate=None):
-    """file_processing.py:80-103 -- list of frame views while len - offset > size."""
-    if transcription_path and frame_rate is None:
-        raise Exception('You must specify frame_rate')
-    if transcription_path:
-        raise NotImplementedError("STM transcript gathering (file_processing.py:87-94) is "
-                                  "outside this build's hot path")
-    frames, offset = [], 0
-    while len(data) - offset > frame_size:
-        frames.append(data[offset:offset + frame_size])
-        offset += step
-    return frames
+    """file_processing.py:80-103 -- list of frame views while len - offset >
+    size (with the STM segment gathering of :87-94, see vad_amd.dataset)."""
+    from .dataset import split_into_frames as _split
+    return _split(data, frame_size, step, transcription_path, frame_rate)
 
 
 class VadPipeline:
