@@ -192,6 +192,22 @@ int64_t vad_format_csv_rows(const float* rows, int64_t n_rows, int32_t n_cols, d
                             char* buf, int64_t buf_size);
 
 /* ---------------------------------------------------------------------------
+ * Energy / ZCR / spectral analyser (realtime_analysis/simple_analyzer.py,
+ * SimpleAnalyser): per-frame features in fp64, out[f*(3+n_bands) + i]:
+ *   0  stEnergy(frame)                    = sum x^2 / frame_len
+ *   1  stZCR(frame) * frame_len           (:210-215)
+ *   2  np.std(|fft|) over all fft_len bins (:203-208)
+ *   3+b stEnergy(|fft|[b*band_bins : (b+1)*band_bins])   (:171-197)
+ * |fft| = |DFT_fft_len([zeros(pad), frame, zeros(pad)])| with
+ * fft_len = frame_len + 2*pad (<= 1024) (:386-400; pad 0: the frame itself).
+ * stEnergy / stZCR are pyAudioAnalysis's (restated; the package is absent).
+ * Frames are frames + f*frame_stride (fp32 samples, exact for int16 audio).
+ * ------------------------------------------------------------------------- */
+int vad_simple_features(const float* frames, int64_t n_frames, int32_t frame_len,
+                        int64_t frame_stride, int32_t fft_len, int32_t pad, int32_t band_bins,
+                        int32_t n_bands, double* out, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Streaming: S independent analyser streams advanced by one frame each
  * (SKLearnAnalyzer.feed_frame, sklearn_analyser.py:46-82, for S streams at
  * once).  State lives in device buffers the caller allocates with the sizes

@@ -47,6 +47,8 @@ SIGNATURES = {
     "vad_tree_plan_destroy": (c_int, [c_vp]),
     "vad_tree_predict": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "vad_features_tree": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "vad_simple_features": (c_int, [c_vp, c_i64, c_i32, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp,
+                                    c_vp]),
     "vad_scale_workspace_bytes": (c_sz, []),
     "vad_scale_features": (c_int, [c_vp, c_i64, c_i32, c_vp, c_sz, c_vp]),
     "vad_format_csv_rows": (c_i64, [c_vp, c_i64, c_i32, ctypes.c_double, c_vp, c_i64]),

@@ -350,6 +350,19 @@ int vad_features_tree(const vad_tree_plan* t, const float* mfcc, int64_t n_frame
                                   (hipStream_t)stream);
 }
 
+int vad_simple_features(const float* frames, int64_t n_frames, int32_t frame_len,
+                        int64_t frame_stride, int32_t fft_len, int32_t pad, int32_t band_bins,
+                        int32_t n_bands, double* out, void* stream) {
+  if (n_frames < 0 || frame_len < 2 || pad < 0 || frame_stride < 0 || band_bins < 1 || n_bands < 0)
+    return VAD_EINVAL;
+  if (fft_len != frame_len + 2 * pad || fft_len > 1024 || n_bands * band_bins > fft_len)
+    return VAD_EUNSUPPORTED;
+  if (n_frames == 0) return VAD_OK;
+  if (!frames || !out) return VAD_EINVAL;
+  return (int)launch_simple_features(frames, n_frames, frame_len, frame_stride, fft_len, pad,
+                                     band_bins, n_bands, out, (hipStream_t)stream);
+}
+
 size_t vad_scale_workspace_bytes(void) { return scale_workspace_bytes(); }
 
 int vad_scale_features(float* rows, int64_t n_rows, int32_t mfcc_n, void* workspace,

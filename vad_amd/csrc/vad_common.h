@@ -70,6 +70,9 @@ hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring
                              int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st);
 hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
                            hipStream_t st);
+hipError_t launch_simple_features(const float* frames, int64_t n_frames, int frame_len,
+                                  int64_t frame_stride, int L, int pad, int band_bins, int n_bands,
+                                  double* out, hipStream_t st);
 size_t scale_workspace_bytes();
 hipError_t launch_scale_features(float* x, int64_t n_rows, int mfcc_n, double* ws, hipStream_t st);
 int64_t format_csv_rows(const float* rows, int64_t n_rows, int n_cols, double label, char* buf,
