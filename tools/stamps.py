@@ -20,7 +20,7 @@ for _ in range(3):
     pipe.mfcc(audio, out=out)
 torch.cuda.synchronize()
 st = out.reshape(-1).view(torch.int64)[: 256 * 8 * 8 * 16].cpu().numpy().reshape(256, 8, 8, 16)
-waves = range(8) if os.environ["VAD_DIAG"] == "5" else range(4)
+waves = range(8) if os.environ["VAD_DIAG"] in ("5", "8") else range(4)
 st = st[:, list(waves), 1:7, :11]  # skip the first tile (cold), keep tiles 1..6
 d = np.diff(st.astype(np.float64), axis=-1)  # 10 intervals
 names = ["stageA_A", "xposeA", "stageA_B", "finish_A", "xposeB", "finish_B", "phase2b", "bar1",

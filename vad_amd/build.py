@@ -45,8 +45,11 @@ def needs_build():
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=True):
-    if not force and not needs_build():
+def build(force=False, verbose=True, defines=(), out=None):
+    """Build the library; ``defines`` / ``out`` make an experiment variant
+    (e.g. ``-DVAD_SPLIT_LOADS=0`` into lib/libvad_amd_<name>.so)."""
+    lib = out or LIB
+    if out is None and not force and not needs_build():
         return LIB
     os.makedirs(LIB_DIR, exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -54,23 +57,29 @@ def build(force=False, verbose=True):
             "-Wno-unused-function"]
     procs, objs = [], []
     for name in SOURCES:  # one object per unit, compiled in parallel
-        obj = os.path.join(LIB_DIR, name.replace(".hip", ".o"))
-        cmd = base + UNIT_FLAGS.get(name, []) + ["-c", os.path.join(CSRC, name), "-o", obj]
+        obj = os.path.join(LIB_DIR, os.path.basename(lib) + "." + name.replace(".hip", ".o"))
+        cmd = base + list(defines) + UNIT_FLAGS.get(name, []) + ["-c", os.path.join(CSRC, name), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
         objs.append(obj)
     if any(p.wait() != 0 for p in procs):
         raise subprocess.CalledProcessError(1, "hipcc -c")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp"] + objs
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
+    os.replace(lib + ".tmp", lib)
     for obj in objs:
         os.remove(obj)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    args = sys.argv[1:]
+    if "--variant" in args:  # python -m vad_amd.build --variant NAME -DX=1 ...
+        name = args[args.index("--variant") + 1]
+        build(defines=[a for a in args if a.startswith("-D")],
+              out=os.path.join(LIB_DIR, f"libvad_amd_{name}.so"))
+    else:
+        build(force="--force" in args)

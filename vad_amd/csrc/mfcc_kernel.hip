@@ -49,19 +49,39 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 // Sample loads by input type: fp32, or int16 PCM (the reference reads int16
 // audio and converts with astype(float32), vad.py:37 / file_processing.py:26-35;
 // the conversion is exact, so both inputs give identical spectra).
+#ifndef VAD_NO_STORE
+#define VAD_NO_STORE 0  // diagnostic builds only: MFCC results are not written
+#endif
+#ifndef VAD_NT_LOADS
+#define VAD_NT_LOADS 0
+#endif
 template <typename TIN>
 struct Samples;
 template <>
 struct Samples<float> {
   static constexpr int kPairAlign = 8;  // bytes for one aligned 2-sample load
-  __device__ static v2f pair(const float* p) { return *reinterpret_cast<const v2f*>(p); }
+  __device__ static v2f pair(const float* p) {
+#if VAD_NT_LOADS == 2
+    const unsigned long long b = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_bit_cast(v2f, b);
+#elif VAD_NT_LOADS
+    return __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p));
+#else
+    return *reinterpret_cast<const v2f*>(p);
+#endif
+  }
   __device__ static float one(const float* p) { return *p; }
 };
 template <>
 struct Samples<int16_t> {
   static constexpr int kPairAlign = 4;
   __device__ static v2f pair(const int16_t* p) {
+#if VAD_NT_LOADS
+    const int v = __builtin_nontemporal_load(reinterpret_cast<const int*>(p));
+#else
     const int v = *reinterpret_cast<const int*>(p);
+#endif
     return (v2f){(float)(int16_t)(v & 0xffff), (float)(v >> 16)};
   }
   __device__ static float one(const int16_t* p) { return (float)*p; }
@@ -74,12 +94,21 @@ struct Samples<int16_t> {
 // pad_stage_a, at first use.  LEN > 0 fixes the frame length at compile time
 // (400 for clips); VEC2 (pair-aligned frames of even length) loads a sample
 // pair per load.
-template <typename TIN, int NZ, bool VEC2, int LEN>
+#ifndef VAD_SPLIT_LOADS
+#define VAD_SPLIT_LOADS 1
+#endif
+constexpr bool kSplitLoads = VAD_SPLIT_LOADS != 0;
+#ifndef VAD_PAIR_FRAMES
+#define VAD_PAIR_FRAMES 1
+#endif
+constexpr bool kPairFrames = VAD_PAIR_FRAMES != 0;
+
+template <typename TIN, int NZ, bool VEC2, int LEN, int B = 0, int E = NZ>
 __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len_rt, int n2,
                                              v2f (&u)[NZ]) {
   const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
-  for (int n1 = 0; n1 < NZ; ++n1) {
+  for (int n1 = B; n1 < (E < NZ ? E : NZ); ++n1) {
     const int t = 32 * n1 + 2 * n2;
     if constexpr (VEC2) {
       const int tc = t < len - 2 ? t : len - 2;
@@ -92,8 +121,8 @@ __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len
   }
 }
 
-template <int NZ, int LEN>
-__device__ __forceinline__ void pad_stage_a(int len_rt, int n2, v2f (&u)[NZ]) {
+template <int NZ, int LEN, int NU = NZ>
+__device__ __forceinline__ void pad_stage_a(int len_rt, int n2, v2f (&u)[NU]) {
   const int len = LEN > 0 ? LEN : len_rt;
 #pragma unroll
   for (int n1 = 0; n1 < NZ; ++n1) {
@@ -159,6 +188,36 @@ __device__ __forceinline__ void stage_a(v2f (&u_in)[NZ], int len, const LaneCons
   pad_stage_a<NZ, LEN>(len, j, u_in);
 #pragma unroll
   for (int n = 0; n < NZ; ++n) u[n] = u_in[n];
+  pk::dft16<NZ>(u);
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
+}
+
+// Paired frames (hop = 32 HOPC samples): chunk c of frame F + 1 is chunk
+// c + HOPC of frame F, so one buffer of NZ + HOPC chunks, buf[c] =
+// (x[32 c + 2 n2], x[32 c + 2 n2 + 1]) from frame F's start, feeds both
+// frames.  Chunks that can reach past frame F's LEN samples clamp their
+// offset to lim (frame F + 1's last pair, or frame F's when F + 1 does not
+// exist), so no load leaves the signal; pad_stage_a zeroes what each frame
+// does not own.
+template <typename TIN, int B, int E, int LEN, int NB>
+__device__ __forceinline__ void load_chunks(const TIN* __restrict__ base, int lim, int n2,
+                                            v2f (&buf)[NB]) {
+#pragma unroll
+  for (int c = B; c < E; ++c) {
+    int o = 32 * c + 2 * n2;
+    if (32 * c + 30 > LEN - 2) o = o < lim ? o : lim;
+    buf[c] = Samples<TIN>::pair(base + o);
+  }
+}
+
+// stage A of the frame whose chunk n1 is buf[OFF + n1]
+template <int NZ, int LEN, int OFF, int NB>
+__device__ __forceinline__ void stage_a_at(const v2f (&buf)[NB], const LaneConsts& L, int j,
+                                           v2f (&u)[16]) {
+#pragma unroll
+  for (int n = 0; n < NZ; ++n) u[n] = buf[OFF + n];
+  pad_stage_a<NZ, LEN, 16>(LEN, j, u);
   pk::dft16<NZ>(u);
 #pragma unroll
   for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
@@ -401,7 +460,8 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
-template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0>
+// HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
@@ -435,6 +495,106 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       __syncthreads();  // log-mel rows complete; P free
       if (wave < kDctGroups) phase2b<SPEC>(plan, lm, wave, lane, f0, n_frames, mfcc_n, out);
     }
+  } else if constexpr (HOPC > 0) {
+    // Lane group grp runs frames F = f0 + 2 grp (pass 0) and F + 1 (pass 1)
+    // from one NZ + HOPC chunk buffer: 18 sample-pair loads per group and
+    // tile instead of 26 (the texture path, not HBM, limits the loads: the
+    // frames overlap 2.5x).  The next tile's chunks are issued in three
+    // batches as the buffer frees up: 0..HOPC-1 after pass 0's stage A,
+    // the rest after pass 1's, split around pass 0's finish.
+    static_assert(LEN > 0 && VEC2, "paired frames need the fixed frame length");
+    constexpr int NB = NZ + HOPC;
+    v2f* gscr = scr + grp * kGroupScratch;
+    LaneConsts L;
+    lane_consts(plan, j, L);
+    const int64_t flast = n_frames - 1;
+    auto pair_base = [&](int64_t t, int& lim) {
+      const int64_t F = t * kTile + 2 * grp;
+      lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
+      return src + (F < flast ? F : flast) * frame_stride;
+    };
+    const int64_t per = (n_tiles + gridDim.x - 1) / gridDim.x;
+    const int64_t t_end = ((int64_t)blockIdx.x + 1) * per < n_tiles ? ((int64_t)blockIdx.x + 1) * per : n_tiles;
+    int64_t tile = (int64_t)blockIdx.x * per;
+    v2f buf[NB];
+    {
+      int lim;
+      const TIN* b0 = pair_base(tile, lim);
+      load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    int64_t prev_f0 = -1;
+    unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
+    (void)stamps;
+    int it = 0;
+    for (; tile < t_end; ++tile, ++it) {
+      unsigned long long st_[kStamps];
+      (void)st_;
+      const int64_t f0 = tile * kTile;
+      const int64_t fa = f0 + 2 * grp, fb = fa + 1;
+      float* prow_a;
+      float* prow_b;
+      if constexpr (MODE == kAudioToSpec) {
+        prow_a = out + (fa < n_frames ? fa : flast) * kBins;
+        prow_b = out + (fb < n_frames ? fb : flast) * kBins;
+      } else {
+        prow_a = P + (2 * grp) * kPStride;
+        prow_b = P + (2 * grp + 1) * kPStride;
+      }
+      int lim;
+      const TIN* nb = pair_base(tile + 1, lim);
+      v2f u[16], col[32];
+      VAD_STAMP(0);
+      stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+      VAD_STAMP(1);
+      __builtin_amdgcn_sched_barrier(0);
+      load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+      __builtin_amdgcn_sched_barrier(0);
+      store_a(u, gscr, j);
+      read_b(L, gscr, col);
+      __builtin_amdgcn_sched_barrier(0);
+      VAD_STAMP(2);
+      // pass 1's stage A covers the latency of pass 0's transpose reads
+      stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
+      __builtin_amdgcn_sched_barrier(0);
+      load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
+      __builtin_amdgcn_sched_barrier(0);
+      VAD_STAMP(3);
+      if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+      __builtin_amdgcn_sched_barrier(0);
+      load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+      __builtin_amdgcn_sched_barrier(0);
+      VAD_STAMP(4);
+      store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
+      read_b(L, gscr, col);
+      VAD_STAMP(5);
+      if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+      if constexpr (MODE == kAudioToMfcc) {
+        __builtin_amdgcn_sched_barrier(0);
+        VAD_STAMP(6);
+        if (prev_f0 >= 0 && wave < kDctGroups)
+          phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        VAD_STAMP(7);
+        lds_barrier();  // P complete; log-mel rows consumed
+        VAD_STAMP(8);
+        phase2a<SPEC>(plan, P, lm, wave, lane);
+        VAD_STAMP(9);
+        lds_barrier();  // log-mel rows complete; P and the FFT scratch free
+        VAD_STAMP(10);
+        prev_f0 = f0;
+        if constexpr (DIAG >= 5) {
+          if (lane == 0 && it < 8) {
+#pragma unroll
+            for (int k = 0; k < kStamps; ++k)
+              stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 16 + k] = st_[k];
+          }
+        }
+      }
+    }
+    if constexpr (MODE == kAudioToMfcc) {
+      if (prev_f0 >= 0 && wave < kDctGroups)
+        phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+    }
   } else {
     v2f* gscr = scr + grp * kGroupScratch;
     LaneConsts L;
@@ -443,11 +603,14 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // the current pass computes
     v2f bufA[NZ], bufB[NZ];
     const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
-    auto load_pass = [&](int64_t t, int pass, v2f (&buf)[NZ]) {
+    auto pass_src = [&](int64_t t, int pass) {
       if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
       int64_t f = t * kTile + pass * kGroups + grp;
       f = f < flast ? f : flast;
-      load_stage_a<TIN, NZ, VEC2, LEN>(src + f * frame_stride, len, j, buf);
+      return src + f * frame_stride;
+    };
+    auto load_pass = [&](int64_t t, int pass, v2f (&buf)[NZ]) {
+      load_stage_a<TIN, NZ, VEC2, LEN>(pass_src(t, pass), len, j, buf);
     };
     // each workgroup owns a contiguous run of tiles: consecutive tiles are
     // adjacent in memory (shared halo in this XCD's L2, page-local loads)
@@ -488,7 +651,37 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       const bool work = DIAG != 6 || wave < 4;
       VAD_STAMP(0);
       v2f u[16], col[32];
-      if (work) {
+      if (work && LEN > 0 && kSplitLoads && DIAG < 5) {
+        // the next tile's sample loads go out in chunks spread over the
+        // tile: a wave's 13 back-to-back pair loads (x 8 waves) would fill
+        // the texture address queue and hold every wave at its load burst
+        const TIN* sa = pass_src(tile + 1, 0);
+        const TIN* sb = pass_src(tile + 1, 1);
+        stage_a<NZ, LEN>(bufA, len, L, j, u);
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage_a<TIN, NZ, VEC2, LEN, 0, 5>(sa, len, j, bufA);
+        __builtin_amdgcn_sched_barrier(0);
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage_a<TIN, NZ, VEC2, LEN, 5, 9>(sa, len, j, bufA);
+        __builtin_amdgcn_sched_barrier(0);
+        stage_a<NZ, LEN>(bufB, len, L, j, u);
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage_a<TIN, NZ, VEC2, LEN, 9, NZ>(sa, len, j, bufA);
+        load_stage_a<TIN, NZ, VEC2, LEN, 0, 4>(sb, len, j, bufB);
+        __builtin_amdgcn_sched_barrier(0);
+        if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage_a<TIN, NZ, VEC2, LEN, 4, 8>(sb, len, j, bufB);
+        __builtin_amdgcn_sched_barrier(0);
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
+        if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+        __builtin_amdgcn_sched_barrier(0);
+        load_stage_a<TIN, NZ, VEC2, LEN, 8, NZ>(sb, len, j, bufB);
+        __builtin_amdgcn_sched_barrier(0);
+      } else if (work) {
         stage_a<NZ, LEN>(bufA, len, L, j, u);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -529,7 +722,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // first (waves 0..3 are older and win VALU arbitration on their
         // SIMD) while their SIMD partners are still in their FFT
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG < 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+          phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -549,7 +742,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     }
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG < 5>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -567,7 +760,8 @@ static int num_cus() {
   return n;
 }
 
-template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0>
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0,
+          int HOPC = 0>
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
@@ -577,12 +771,12 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG>),
+        reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>),
         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG>), dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>), dim3(grid), dim3(kThreads),
                      smem, st, plan, src, stride, len, n, out);
   return hipGetLastError();
 }
@@ -596,13 +790,22 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
-      if (diag == 5) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 5 && stride == 160 && kPairFrames)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 5, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 5 || diag == 8) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
       if (diag == 6) return launch_t<TIN, MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
       if (diag == 7) return launch_t<TIN, MODE, 13, true, 400, 1, 7>(plan, src, stride, len, n, out, st);
+      if (stride == 160 && kPairFrames)  // the reference hop (config.py:22)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
-    if (MODE == kAudioToMfcc && spec == 2)
+    if (MODE == kAudioToMfcc && spec == 2) {
+      if (stride == 160 && kPairFrames)
+        return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5>(plan, src, stride, len, n, out, st);
       return launch_t<TIN, MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
+    }
+    if (stride == 160 && kPairFrames)
+      return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5>(plan, src, stride, len, n, out, st);
     return launch_t<TIN, MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
   }
   if (used <= 32 * 13) {
