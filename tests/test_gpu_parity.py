@@ -212,6 +212,24 @@ def test_ffn_generic_topology(torch_cuda):
         np.testing.assert_array_equal(got[ok], ref[ok])
 
 
+def test_ffn_split_f16_rescale(torch_cuda, golden):
+    """Window labels of networks whose activations overflow f16: the split-f16
+    MFMA path reruns such tiles at a power-of-two scale.  Scaling layer l's
+    weights by 2^10 and its bias by 2^(10 (l + 1)) scales every activation by
+    a power of two, so the labels are the unscaled network's."""
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    w = golden("ffn")
+    clip = torch_cuda.from_numpy(w["test_clip"]).cuda()
+    m = VadPipeline().mfcc(clip)
+    for prefix, n in (("ref39", 4), ("bl13", 3)):
+        lay = [(W * 2.0 ** 10, b * 2.0 ** (10 * (i + 1)))
+               for i, (W, b) in enumerate(layers_from(w, prefix, n))]
+        got = FFNClassifier(lay).plan.window_labels(m).cpu().numpy()
+        sure = w[f"test_margin_{prefix}"] > MARGIN_TOL
+        np.testing.assert_array_equal(got[sure], w[f"test_labels_{prefix}"][sure])
+
+
 def test_analyser_features_and_labels_on_clip(torch_cuda, golden, fb26):
     """Whole-clip analyser windows: GPU features/labels vs the oracle."""
     from vad_amd import plan as P

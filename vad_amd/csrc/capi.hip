@@ -40,6 +40,7 @@ static bool matches_table(const MfccDev& h) {
 struct vad_ffn_plan {
   FfnDev net;        // by-value kernel argument, frag -> device buffer
   float* frag_dev;
+  uint32_t* fragh_dev;  // split-f16 weights (null when the topology has none)
 };
 
 #define VAD_TRY(x)                          \
@@ -261,6 +262,39 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
     for (int c = 0; c < 4; ++c) push_slot([&](int, int) { return b_at(l, c); });
   }
 
+  // split-f16 weights for the specialised topologies (ffn_kernel.hip
+  // dense_h3): W = hi + lo, both f16 (RNE), per (layer l, tile mt, K-step s)
+  // a hi slot and a lo slot of 8 halves per lane.  A[i][k] with row i = lane
+  // & 15 -> output unit 16 mt + i and k = 8 (lane >> 4) + q -> input unit
+  // 32 s + k at layer 0, else 16 (2 s + (q >> 2)) + 4 (lane >> 4) + (q & 3):
+  // the previous layer's accumulator rows as the lane holds them.
+  std::vector<uint32_t> fragh;
+  const bool use_h3 = (ref39 || bl13) && !getenv("VAD_FFN_EXACT");
+  if (use_h3) {
+    const int hl = bl13 ? n_layers - 1 : n_layers;  // bl13's output layer stays on the VALU
+    for (int l = 0; l < hl; ++l) {
+      const int ks = l == 0 ? (dims[0] + 31) / 32 : (tiles[l - 1] + 1) / 2;
+      for (int mt = 0; mt < tiles[l]; ++mt)
+        for (int s = 0; s < ks; ++s)
+          for (int part = 0; part < 2; ++part)
+            for (int lane = 0; lane < 64; ++lane) {
+              const int i = lane & 15, g = lane >> 4;
+              _Float16 h[8];
+              for (int q = 0; q < 8; ++q) {
+                const int k = l == 0 ? 32 * s + 8 * g + q
+                                     : 16 * (2 * s + (q >> 2)) + 4 * g + (q & 3);
+                const bool in_range = l == 0 || 2 * s + (q >> 2) < tiles[l - 1];
+                const float w = in_range ? w_at(l, k, 16 * mt + i) : 0.f;
+                const _Float16 hi = (_Float16)w;
+                h[q] = part == 0 ? hi : (_Float16)(w - (float)hi);
+              }
+              uint32_t word[4];
+              memcpy(word, h, sizeof(word));
+              for (int q = 0; q < 4; ++q) fragh.push_back(word[q]);
+            }
+    }
+  }
+
   vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));
   if (!p) return VAD_ENOMEM;
   hipError_t e = hipMalloc((void**)&p->frag_dev, frag.size() * sizeof(float));
@@ -268,6 +302,19 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   e = hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(float), hipMemcpyHostToDevice);
   if (e != hipSuccess) { (void)hipFree(p->frag_dev); free(p); return (int)e; }
   net.frag = p->frag_dev;
+  net.fragh = nullptr;
+  if (!fragh.empty()) {
+    e = hipMalloc((void**)&p->fragh_dev, fragh.size() * sizeof(uint32_t));
+    if (e == hipSuccess)
+      e = hipMemcpy(p->fragh_dev, fragh.data(), fragh.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(p->fragh_dev);
+      (void)hipFree(p->frag_dev);
+      free(p);
+      return (int)e;
+    }
+    net.fragh = p->fragh_dev;
+  }
   p->net = net;
   *out = p;
   return VAD_OK;
@@ -276,6 +323,7 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
 int vad_ffn_plan_destroy(vad_ffn_plan* p) {
   if (!p) return VAD_OK;
   (void)hipFree(p->frag_dev);
+  if (p->fragh_dev) (void)hipFree(p->fragh_dev);
   free(p);
   return VAD_OK;
 }

@@ -112,11 +112,16 @@ struct Topo {
 };
 
 // Load the per-lane weight fragments a network keeps in VGPRs.
-template <class TP>
-__device__ __forceinline__ void load_frags(const float* __restrict__ frag, int lane, float (&fa)[TP::NA],
-                                           float (&fb)[TP::NB], float (&fv)[TP::NV + TP::NVB + 1]) {
+template <class TP, bool NO_A = false>
+__device__ __forceinline__ void load_frags(const float* __restrict__ frag, int lane,
+                                           float (&fa)[NO_A ? 1 : TP::NA], float (&fb)[TP::NB],
+                                           float (&fv)[TP::NV + TP::NVB + 1]) {
+  if constexpr (NO_A) {
+    fa[0] = 0.f;
+  } else {
 #pragma unroll
-  for (int s = 0; s < TP::NA; ++s) fa[s] = frag[s * 64 + lane];
+    for (int s = 0; s < TP::NA; ++s) fa[s] = frag[s * 64 + lane];
+  }
 #pragma unroll
   for (int s = 0; s < TP::NB; ++s) fb[s] = frag[(TP::NA_ALL + s) * 64 + lane];
   constexpr int v0 = TP::NA_ALL + TP::NB;
@@ -133,8 +138,8 @@ __device__ __forceinline__ void load_frags(const float* __restrict__ frag, int l
 // VALU output layer: lane (g, window jw) holds hidden units 16t + 4g + r of
 // its window; each class is a 16-term partial sum per lane, completed across
 // the four lane groups (xor 16, xor 32: a fixed association, deterministic).
-template <class TP, int TI>
-__device__ __forceinline__ f32x4 valu_out_layer(const float* __restrict__ fv, const f32x4 (&h)[TI]) {
+template <class TP, int TI, class FV = const float*>
+__device__ __forceinline__ f32x4 valu_out_layer(FV fv, const f32x4 (&h)[TI], float bias_scale = 1.f) {
   constexpr int NC = TP::NVB;
   f32x4 z = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
@@ -151,7 +156,7 @@ __device__ __forceinline__ f32x4 valu_out_layer(const float* __restrict__ fv, co
     float p = p0 + p1;
     p += __shfl_xor(p, 16);
     p += __shfl_xor(p, 32);
-    z[c] = p + fv[TP::NV + c];
+    z[c] = p + fv[TP::NV + c] * bias_scale;
   }
   return z;
 }
@@ -193,6 +198,205 @@ __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const
       else {
         f32x4 h4[T4];
         dense_layer<T4, T3>(fa + TP::A0 + TP::A1 + TP::A2, fb + 4 * (T1 + T2 + T3), h3, h4, false);
+        return h4[0];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Split-f16 MFMA forward (the specialised topologies): every GEMM operand is
+// split as v = hi + lo with hi = f16(v), lo = f16(v - hi) (RNE), and a layer
+// accumulates lo*hi + hi*lo + hi*hi on v_mfma_f32_16x16x32_f16 (f32
+// accumulate; the dropped lo*lo term is ~2^-22 of a product).  16x16x32
+// f16 takes 16 cycles against 32 for 16x16x4 f32 at 8x the K: the three
+// products cost 3/16 of the exact-f32 MFMA time.  f16 holds |v| < 65504
+// (NaN passes through as NaN): a tile with a larger layer input reruns on
+// the exact f32 path.
+// Operand layout (16x16x32): A lane (g, i) holds A[i][8g + q], B lane (g, j)
+// holds B[8g + q][j], q = 0..7; D lane (g, j) holds D[4g + r][j].  The K
+// order inside a K-step is the host's (capi.hip fragh): layer 0 k = input
+// 32 s + 8g + q; later layers take the previous accumulator tiles 2s and
+// 2s + 1 as the lane holds them, so no lane exchange between layers.
+// ---------------------------------------------------------------------------
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr float kH3Max = 65504.f;  // largest finite f16
+
+__device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+  u4 hw, lw;
+#pragma unroll
+  for (int q = 0; q < 8; q += 2) {
+    const f2 p = {v[q], v[q + 1]};
+    const h2 h = __builtin_convertvector(p, h2);
+    const h2 r = __builtin_convertvector(p - __builtin_convertvector(h, f2), h2);
+    hw[q / 2] = __builtin_bit_cast(unsigned, h);
+    lw[q / 2] = __builtin_bit_cast(unsigned, r);
+  }
+  hi = __builtin_bit_cast(h8, hw);
+  lo = __builtin_bit_cast(h8, lw);
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Scale of one layer's inputs (wave-uniform): 1 while every |input| fits
+// f16 (NaN passes through f16 as NaN and does not count), else the power of
+// two that brings the wave's largest into [2^14, 2^15) -- the inputs are
+// scaled in place and the layer unscales its result exactly.
+template <int K>
+__device__ __forceinline__ float layer_scale(float (&v)[K][8]) {
+  float m = 0.f;
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+#pragma unroll
+    for (int q = 0; q < 8; q += 2)
+      m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(v[s][q]), __builtin_fabsf(v[s][q + 1])));
+  if (__builtin_amdgcn_ballot_w64(m >= kH3Max) == 0) return 1.f;
+  m = wave_max(m);
+  if (!(m < INFINITY)) return 1.f;  // inf stays inf (-> NaN logits, class 0)
+  // m >= 65504 is a normal float: 2^(14 - exponent(m)), built from its bits
+  const int e = (int)((__builtin_bit_cast(unsigned, m) >> 23) & 0xff) - 127;
+  const float sc = __builtin_bit_cast(float, (unsigned)(127 + 14 - e) << 23);
+#pragma unroll
+  for (int s = 0; s < K; ++s)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[s][q] *= sc;
+  return sc;
+}
+
+// Layer inputs after a layer with TI accumulator tiles: K-step s takes tiles
+// 2s and 2s + 1 as the lane holds them.
+template <int TI>
+__device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1) / 2][8]) {
+#pragma unroll
+  for (int s = 0; s < (TI + 1) / 2; ++s)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[s][q] = h[2 * s][q];
+      v[s][q + 4] = 2 * s + 1 < TI ? h[2 * s + 1][q] : 0.f;
+    }
+}
+
+// out[mt] = bias + sum_s lo*hi + hi*lo + hi*hi (small terms first) on inputs
+// v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
+template <int TO, int KS, class FB>
+__device__ __forceinline__ void dense_h3(const u4 (&A)[TO * KS][2], FB b, float (&v)[KS][8],
+                                         f32x4 (&out)[TO], bool relu) {
+  const float sc = layer_scale<KS>(v);
+  h8 bh[KS], bl[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
+  f32x4 acc[TO];
+#pragma unroll
+  for (int mt = 0; mt < TO; ++mt) acc[mt] = (f32x4){b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
+  if (sc != 1.f) {
+#pragma unroll
+    for (int mt = 0; mt < TO; ++mt) acc[mt] *= sc;
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int mt = 0; mt < TO; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][1]), bh[s],
+                                                       acc[mt], 0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int mt = 0; mt < TO; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bl[s],
+                                                       acc[mt], 0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int mt = 0; mt < TO; ++mt)
+      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bh[s],
+                                                       acc[mt], 0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  if (sc != 1.f) {
+    const float inv = 1.f / sc;  // exact: a power of two
+#pragma unroll
+    for (int mt = 0; mt < TO; ++mt) acc[mt] *= inv;
+  }
+#pragma unroll
+  for (int mt = 0; mt < TO; ++mt) {
+    f32x4 o = acc[mt];
+    if (relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = relu_nan(o[r]);
+    }
+    out[mt] = o;
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// Split-f16 shape of a Topo: K-steps per layer and fragment slots.
+template <class TP, int KS0, int T1, int T2, int T3, int T4>
+struct HTopo {
+  static constexpr int HL = TP::VL ? TP::NL - 1 : TP::NL;  // layers on split-f16 MFMA
+  static constexpr int K0 = (4 * KS0 + 31) / 32;
+  static constexpr int K1 = (T1 + 1) / 2, K2 = (T2 + 1) / 2, K3 = (T3 + 1) / 2;
+  static constexpr int S0 = T1 * K0;
+  static constexpr int S1 = HL > 1 ? T2 * K1 : 0;
+  static constexpr int S2 = HL > 2 ? T3 * K2 : 0;
+  static constexpr int S3 = HL > 3 ? T4 * K3 : 0;
+  static constexpr int NS = S0 + S1 + S2 + S3;
+};
+
+template <class HP>
+__device__ __forceinline__ void load_fragh(const uint32_t* __restrict__ fragh, int lane, u4 (&fh)[HP::NS][2]) {
+  const u4* f = reinterpret_cast<const u4*>(fragh);
+#pragma unroll
+  for (int sl = 0; sl < HP::NS; ++sl) {
+    fh[sl][0] = f[(2 * sl) * 64 + lane];
+    fh[sl][1] = f[(2 * sl + 1) * 64 + lane];
+  }
+}
+
+template <int N, int OFF, int M>
+__device__ __forceinline__ const u4 (&frag_slice(const u4 (&fh)[M][2]))[N][2] {
+  return *reinterpret_cast<const u4(*)[N][2]>(&fh[OFF]);
+}
+
+// Forward of one 16-window tile: x0 holds the layer-0 inputs of K-step s,
+// k = 8g + q (g = lane >> 4).
+template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV>
+__device__ __forceinline__ f32x4 mlp_forward_h3(const u4 (&fh)[HTopo<Topo<KS0, T1, T2, T3, T4, NC>, KS0, T1, T2, T3, T4>::NS][2],
+                                                FB fb, FV fv, float (&x0)[(4 * KS0 + 31) / 32][8]) {
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
+  using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+  f32x4 h1[T1];
+  dense_h3<T1, HP::K0, FB>(frag_slice<HP::S0, 0>(fh), fb, x0, h1, TP::NL > 1);
+  if constexpr (TP::NL == 1) return h1[0];
+  else if constexpr (TP::NL == 2 && TP::VL) return valu_out_layer<TP, T1, FV>(fv, h1);
+  else {
+    float v1[HP::K1][8];
+    acts_of<T1>(h1, v1);
+    f32x4 h2[T2];
+    dense_h3<T2, HP::K1, FB>(frag_slice<HP::S1, HP::S0>(fh), fb + 4 * T1, v1, h2, TP::NL > 2);
+    if constexpr (TP::NL == 2) return h2[0];
+    else if constexpr (TP::NL == 3 && TP::VL) return valu_out_layer<TP, T2, FV>(fv, h2);
+    else {
+      float v2[HP::K2][8];
+      acts_of<T2>(h2, v2);
+      f32x4 h3[T3];
+      dense_h3<T3, HP::K2, FB>(frag_slice<HP::S2, HP::S0 + HP::S1>(fh), fb + 4 * (T1 + T2), v2, h3,
+                               TP::NL > 3);
+      if constexpr (TP::NL == 3) return h3[0];
+      else if constexpr (TP::VL) return valu_out_layer<TP, T3, FV>(fv, h3);
+      else {
+        float v3[HP::K3][8];
+        acts_of<T3>(h3, v3);
+        f32x4 h4[T4];
+        dense_h3<T4, HP::K3, FB>(frag_slice<HP::S3, HP::S0 + HP::S1 + HP::S2>(fh), fb + 4 * (T1 + T2 + T3),
+                                 v3, h4, false);
         return h4[0];
       }
     }
@@ -246,21 +450,24 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 }
 
 // Windows of an MFCC sequence, 64 per block iteration (4 waves x 16):
-//   A  the 68 MFCC rows the chunk needs are staged in LDS (coalesced);
+//   A  the 68 MFCC rows the chunk needs are staged in LDS (coalesced; loaded
+//      into registers two chunks ahead);
 //   B  every (window, coefficient) feature triple is computed once, by one
-//      thread, from LDS (fp64 window statistics), into an LDS feature tile;
+//      thread, from LDS into an LDS feature tile;
 //   C  each wave runs the MFMA chain on 16 windows with its layer-0 B
 //      operands read from the tile, then the argmax.
+// rows / X are double-buffered, so two barriers per chunk order the phases.
 constexpr int kChunk = 64;
-constexpr int kXStride = 65;  // floats per feature row (64 + 1: bank spread)
+constexpr int kXStride = 68;  // floats per feature row: 16-B aligned, conflict-free b128 reads
 
-template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN>
-__global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float* __restrict__ mfcc,
-                                                         int64_t n_rows, int mfcc_n_rt, int mode,
-                                                         uint8_t* __restrict__ labels) {
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN, bool H3>
+__device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* __restrict__ mfcc,
+                                                int64_t n_rows, int mfcc_n_rt, int mode,
+                                                uint8_t* __restrict__ labels) {
   using TP = Topo<KS0, T1, T2, T3, T4, NC>;
-  __shared__ float rows[(kChunk + 4) * kMaxCoefs];
-  __shared__ float X[kChunk * kXStride];
+  using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+  __shared__ float rows[2][(kChunk + 4) * kMaxCoefs];
+  __shared__ __attribute__((aligned(16))) float X[2][kChunk * kXStride];
   const int mfcc_n = MN > 0 ? MN : mfcc_n_rt;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -270,68 +477,122 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
   const int in_dim = net.dims[0];
   const int nfeat = 3 * mfcc_n;
 
-  float fa[TP::NA];
+  // split-f16 (H3): the f16 weight fragments stay in VGPRs in place of the
+  // f32 ones
+  constexpr int kNA = H3 ? 1 : TP::NA;
+  constexpr int kNH = H3 ? HP::NS : 1;
+  float fa[kNA];
   float fb[TP::NB];
   float fv[TP::NV + TP::NVB + 1];
-  load_frags<TP>(net.frag, lane, fa, fb, fv);
+  u4 fh[kNH][2];
+  if constexpr (H3) {
+    load_frags<TP, true>(net.frag, lane, fa, fb, fv);
+    load_fragh<HP>(net.fragh, lane, fh);
+    // feature columns the layer-0 reads past the features stay 0
+    for (int i = tid; i < 2 * kChunk * kXStride; i += 256) (&X[0][0])[i] = 0.f;
+  } else {
+    load_frags<TP>(net.frag, lane, fa, fb, fv);
+  }
 
   const int64_t n_frames = n_rows + 5;
   const int64_t n_chunks = (n_rows + kChunk - 1) / kChunk;
-  // rows of a chunk: (kChunk + 4) x mfcc_n floats, <= 4 per thread; the next
-  // chunk's are loaded into registers while the current one computes
+  // rows of a chunk: (kChunk + 4) x mfcc_n floats, <= 5 per thread, loaded
+  // two chunks ahead
   constexpr int kRowRegs = ((kChunk + 4) * kMaxCoefs + 255) / 256;
-  float pre[kRowRegs];
-  auto load_rows = [&](int64_t ch) {
+  float pre[2][kRowRegs];
+  auto load_rows = [&](int64_t ch, float (&dst)[kRowRegs]) {
     const int64_t base = ch * kChunk;
     const int64_t avail = ch < n_chunks ? n_frames - base : 0;
     const int nr = (int)(avail < kChunk + 4 ? avail : kChunk + 4);
 #pragma unroll
     for (int q = 0; q < kRowRegs; ++q) {
       const int i = tid + 256 * q;
-      pre[q] = i < nr * mfcc_n ? mfcc[base * mfcc_n + i] : 0.f;
+      dst[q] = i < nr * mfcc_n ? mfcc[base * mfcc_n + i] : 0.f;
     }
   };
-  load_rows(blockIdx.x);
-  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x) {
+  load_rows(blockIdx.x, pre[0]);
+  load_rows(blockIdx.x + gridDim.x, pre[1]);
+  int buf = 0;
+  for (int64_t ch = blockIdx.x; ch < n_chunks; ch += gridDim.x, buf ^= 1) {
     const int64_t base = ch * kChunk;
+    float* rw_ = rows[buf];
+    float* Xb = X[buf];
     // ---- A: rows base .. base+67 (prefetched) ------------------------------
 #pragma unroll
     for (int q = 0; q < kRowRegs; ++q) {
       const int i = tid + 256 * q;
       if (i < (kChunk + 4) * mfcc_n) {
         const int r = i / mfcc_n, c = i - r * mfcc_n;
-        rows[r * kMaxCoefs + c] = pre[q];
+        rw_[r * kMaxCoefs + c] = pre[0][q];
       }
+      pre[0][q] = pre[1][q];
     }
     __syncthreads();
-    load_rows(ch + gridDim.x);
+    load_rows(ch + 2 * (int64_t)gridDim.x, pre[1]);
     // ---- B: features (sklearn_analyser.py:52-69 / file_processing.py:51-66)
     const int64_t nwin64 = n_rows - base;
     const int nwin = (int)(nwin64 < kChunk ? nwin64 : kChunk);
     for (int i = tid; i < nwin * mfcc_n; i += 256) {
       const int w = i / mfcc_n, c = i - w * mfcc_n;
-      const float* rw = rows + w * kMaxCoefs + c;
-      const Feat3 ft = feature_triple(rw[0], rw[kMaxCoefs], rw[2 * kMaxCoefs], rw[3 * kMaxCoefs],
-                                      rw[4 * kMaxCoefs], mode);
-      float* xw = X + w * kXStride;
-      xw[c] = ft.mn;
-      xw[mfcc_n + c] = ft.d1;
-      xw[2 * mfcc_n + c] = ft.d2;
+      const float* r = rw_ + w * kMaxCoefs + c;
+      const Feat3 ft = feature_triple(r[0], r[kMaxCoefs], r[2 * kMaxCoefs], r[3 * kMaxCoefs],
+                                      r[4 * kMaxCoefs], mode);
+      float* xw = Xb + w * kXStride;
+      if constexpr (H3) {  // the split-f16 layer 0 reads every column: unused ones are 0
+        xw[c] = c < in_dim ? ft.mn : 0.f;
+        xw[mfcc_n + c] = mfcc_n + c < in_dim ? ft.d1 : 0.f;
+        xw[2 * mfcc_n + c] = 2 * mfcc_n + c < in_dim ? ft.d2 : 0.f;
+      } else {
+        xw[c] = ft.mn;
+        xw[mfcc_n + c] = ft.d1;
+        xw[2 * mfcc_n + c] = ft.d2;
+      }
     }
     __syncthreads();
     // ---- C: MFMA chain, 16 windows per wave --------------------------------
     const int wl = wv * 16 + jw;
     const int64_t w = base + wl;
-    float x[KS0];
+    f32x4 z;
+    if constexpr (H3) {
+      // windows past nwin read stale (finite) features: computed, not stored
+      float x0[HP::K0][8];
+      const v4f* xr = reinterpret_cast<const v4f*>(Xb + wl * kXStride + 8 * g);
 #pragma unroll
-    for (int s = 0; s < KS0; ++s) {
-      const int f = 4 * s + g;
-      x[s] = (f < in_dim && f < nfeat && wl < nwin) ? X[wl * kXStride + f] : 0.f;
+      for (int s = 0; s < HP::K0; ++s) {
+        const v4f lo4 = xr[8 * s], hi4 = xr[8 * s + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x0[s][q] = lo4[q];
+          x0[s][q + 4] = hi4[q];
+        }
+      }
+      z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(fh, (const float*)fb, (const float*)fv, x0);
+    } else {
+      float x[KS0];
+#pragma unroll
+      for (int s = 0; s < KS0; ++s) {
+        const int f = 4 * s + g;
+        x[s] = (f < in_dim && f < nfeat && wl < nwin) ? Xb[wl * kXStride + f] : 0.f;
+      }
+      z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     }
-    const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     if (g == 0 && wl < nwin) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
-    __syncthreads();
   }
+}
+
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN>
+__global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float* __restrict__ mfcc,
+                                                         int64_t n_rows, int mfcc_n_rt, int mode,
+                                                         uint8_t* __restrict__ labels) {
+  ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, false>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
+}
+
+// split-f16 variant: two 4-wave blocks per CU (<= 256 registers per lane)
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffn_window_h3_kernel(
+    FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, int mfcc_n_rt, int mode,
+    uint8_t* __restrict__ labels) {
+  ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, true>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
 }
 
 // Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
@@ -437,6 +698,16 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
     // so each block loads its weight fragments once and streams its chunks
     const int64_t cap = 2 * ffn_num_cus();
     if (chunks > cap) chunks = cap;
+    // split-f16 MFMA: the two specialised topologies, when the plan has fragh
+    constexpr bool kH3 = (KS0 == 10 && T1 == 4 && T2 == 2 && T3 == 1 && T4 == 1) ||
+                         (KS0 == 4 && T1 == 4 && T2 == 4 && T3 == 1 && T4 == 0);
+    if constexpr (kH3) {
+      if (mfcc_n == 13 && net.fragh) {
+        hipLaunchKernelGGL((ffn_window_h3_kernel<KS0, T1, T2, T3, T4, NC, 13>), dim3((int)chunks),
+                           dim3(256), 0, st, net, in, n_rows, mfcc_n, mode, labels);
+        return hipGetLastError();
+      }
+    }
     if (mfcc_n == 13)
       hipLaunchKernelGGL((ffn_window_kernel<KS0, T1, T2, T3, T4, NC, 13>), dim3((int)chunks), dim3(256), 0,
                          st, net, in, n_rows, mfcc_n, mode, labels);

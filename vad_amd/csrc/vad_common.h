@@ -44,6 +44,9 @@ struct FfnDev {
   int ks0;                        // K-steps of layer 0 = ceil(in_dim / 4) (16 = generic)
   int tiles[VAD_MAX_FFN_LAYERS];  // 16-row output tiles per layer
   const float* frag;              // [slot][64] per-lane fragments: A operands, then biases
+  // split-f16 MFMA weights (ref39 / bl13; null = exact f32 MFMA only):
+  // [slot][64 lanes][4 words] of packed f16, slot = ((layer, mt, s), hi | lo)
+  const uint32_t* fragh;
 };
 
 // Decision-tree node (tree_kernel.hip): internal if feature >= 0 (go left
