@@ -1,0 +1,41 @@
+"""profiles/pmc_traffic.json from a tools/profile.sh run:
+python tools/traffic_json.py gpurun_out/prof_<tag> <tag-note>
+hbm bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024 (gfx950
+FETCH_SIZE counts half of a wide coalesced read: MI355X_MICROARCH.md, HBM
+section), averaged over the timed launches of each kernel."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, note = sys.argv[1], sys.argv[2]
+
+
+def per_kernel(counter):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(f"{d}/**/run_counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter:
+                vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]))
+    return vals
+
+
+fetch = {k: v for k, v in per_kernel("FETCH_SIZE").items()}
+write = {k: v for k, v in per_kernel("WRITE_SIZE").items()}
+algo = {"mfcc_kernel": 692e6, "ffn_window": 53e6}
+out = {"source": note, "correction": "hbm_bytes = 2 * FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE "
+       "reports half of a wide coalesced read, MI355X_MICROARCH.md HBM section)"}
+for key, label in (("mfcc_kernel", "mfcc_kernel"), ("ffn_window", "ffn_kernel")):
+    fk = [k for k in fetch if key in k and "vad::" in k]
+    wk = [k for k in write if key in k and "vad::" in k]
+    if not fk or not wk:
+        continue
+    fv = sum(fetch[fk[0]][2:]) / max(1, len(fetch[fk[0]][2:]))
+    wv = sum(write[wk[0]][2:]) / max(1, len(write[wk[0]][2:]))
+    out[label] = {"kernel": fk[0], "fetch_kib": fv, "write_kib": wv,
+                  "hbm_bytes_per_launch": 2 * fv * 1024 + wv * 1024,
+                  "algorithmic_bytes_per_launch": algo[key]}
+json.dump(out, open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
