@@ -230,6 +230,29 @@ def test_ffn_split_f16_rescale(torch_cuda, golden):
         np.testing.assert_array_equal(got[sure], w[f"test_labels_{prefix}"][sure])
 
 
+def test_window_labels_random_nets_long_clip(torch_cuda):
+    """Window labels of both specialised topologies (split-f16 MFMA path) on a
+    20k-frame synthetic clip with digital silence (NaN windows) vs the
+    oracle's forward on the same device features, where the oracle's top-2
+    margin exceeds 1e-3."""
+    from vad_amd import plan as P
+    from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 20000
+    clip = O.synth_clip(160 * (F - 1) + 401, seed=7).astype(np.float32)
+    for topo in (TOPOLOGY_BL13, TOPOLOGY_REF39):
+        lay = random_layers(topo, seed=3)
+        pipe = VadPipeline(FFNClassifier(lay))
+        m = pipe.mfcc(torch_cuda.from_numpy(clip).cuda())
+        got = pipe.ffn.plan.window_labels(m).cpu().numpy()
+        x = P.window_features(m, 0).cpu().numpy()[:, :topo[0]]
+        ref = O.ffn_labels(x, lay)
+        ok = O.ffn_margin(x, lay) > 1e-3
+        assert np.isnan(x).any(axis=1).sum() > 0  # NaN windows are exercised
+        np.testing.assert_array_equal(got[ok], ref[ok])
+        assert ok.mean() > 0.99
+
+
 def test_analyser_features_and_labels_on_clip(torch_cuda, golden, fb26):
     """Whole-clip analyser windows: GPU features/labels vs the oracle."""
     from vad_amd import plan as P

@@ -253,12 +253,15 @@ __device__ __forceinline__ float wave_max(float v) {
 // scaled in place and the layer unscales its result exactly.
 template <int K>
 __device__ __forceinline__ float layer_scale(float (&v)[K][8]) {
+  // inputs are NaN-free (ffn_window_body masks NaN windows) and VALU
+  // results or LDS reads (never MFMA results, whose read hazard inline asm
+  // would hide): one v_max3 per pair, no canonicalising maxNum sequence
   float m = 0.f;
 #pragma unroll
   for (int s = 0; s < K; ++s)
 #pragma unroll
     for (int q = 0; q < 8; q += 2)
-      m = __builtin_fmaxf(m, __builtin_fmaxf(__builtin_fabsf(v[s][q]), __builtin_fabsf(v[s][q + 1])));
+      asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[s][q]), "v"(v[s][q + 1]));
   if (__builtin_amdgcn_ballot_w64(m >= kH3Max) == 0) return 1.f;
   m = wave_max(m);
   if (!(m < INFINITY)) return 1.f;  // inf stays inf (-> NaN logits, class 0)
@@ -294,43 +297,49 @@ __device__ __forceinline__ void dense_h3(const u4 (&A)[TO * KS][2], FB b, float 
   h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
-  f32x4 acc[TO];
+  auto chain = [&](const f32x4 (&init)[TO], f32x4 (&acc)[TO]) {
 #pragma unroll
-  for (int mt = 0; mt < TO; ++mt) acc[mt] = (f32x4){b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
-  if (sc != 1.f) {
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int mt = 0; mt < TO; ++mt) acc[mt] *= sc;
-  }
+      for (int mt = 0; mt < TO; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][1]), bh[s],
+                                                         s == 0 ? init[mt] : acc[mt], 0, 0, 0);
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int mt = 0; mt < TO; ++mt)
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][1]), bh[s],
-                                                       acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < TO; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bl[s],
+                                                         acc[mt], 0, 0, 0);
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+    for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int mt = 0; mt < TO; ++mt)
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bl[s],
-                                                       acc[mt], 0, 0, 0);
+      for (int mt = 0; mt < TO; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bh[s],
+                                                         acc[mt], 0, 0, 0);
+  };
+  f32x4 bias[TO], acc[TO];
 #pragma unroll
-  for (int s = 0; s < KS; ++s)
+  for (int mt = 0; mt < TO; ++mt) bias[mt] = (f32x4){b[mt * 4 + 0], b[mt * 4 + 1], b[mt * 4 + 2], b[mt * 4 + 3]};
+  if (sc == 1.f) {
+    chain(bias, acc);  // the bias registers are the first MFMA's C operand
+  } else {             // rare: scaled inputs, scaled bias, exact unscale
+    f32x4 sb[TO];
 #pragma unroll
-    for (int mt = 0; mt < TO; ++mt)
-      acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bh[s],
-                                                       acc[mt], 0, 0, 0);
-  __builtin_amdgcn_sched_barrier(0);
-  if (sc != 1.f) {
+    for (int mt = 0; mt < TO; ++mt) sb[mt] = bias[mt] * sc;
+    chain(sb, acc);
     const float inv = 1.f / sc;  // exact: a power of two
 #pragma unroll
     for (int mt = 0; mt < TO; ++mt) acc[mt] *= inv;
   }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int mt = 0; mt < TO; ++mt) {
     f32x4 o = acc[mt];
+    // NaN-free here: clamp to [0, inf) is the ReLU (a builtin, not asm: the
+    // operand is an MFMA result, whose read hazard the compiler must see)
     if (relu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = relu_nan(o[r]);
+      for (int r = 0; r < 4; ++r) o[r] = __builtin_amdgcn_fmed3f(o[r], 0.f, __builtin_inff());
     }
     out[mt] = o;
   }
@@ -457,6 +466,9 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 //   C  each wave runs the MFMA chain on 16 windows with its layer-0 B
 //      operands read from the tile, then the argmax.
 // rows / X are double-buffered, so two barriers per chunk order the phases.
+#ifndef VAD_FFN_DIAG
+#define VAD_FFN_DIAG 0  // diagnostic builds only: 1 skips the features, 2 the MLP
+#endif
 constexpr int kChunk = 64;
 constexpr int kXStride = 68;  // floats per feature row: 16-B aligned, conflict-free b128 reads
 
@@ -466,8 +478,13 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
                                                 uint8_t* __restrict__ labels) {
   using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+  static_assert(!H3 || (MN > 0 && MN * (kChunk / 4) <= 256), "split-f16 needs the sliding feature phase");
   __shared__ float rows[2][(kChunk + 4) * kMaxCoefs];
   __shared__ __attribute__((aligned(16))) float X[2][kChunk * kXStride];
+  // H3: windows with a NaN feature (a flat coefficient) -- their features go
+  // to the MLP as 0 and their logits are set to NaN (class 0), as the
+  // reference's NaN-propagating forward would give
+  __shared__ int wnan[2][kChunk];
   const int mfcc_n = MN > 0 ? MN : mfcc_n_rt;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -527,12 +544,42 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
       }
       pre[0][q] = pre[1][q];
     }
+    if (H3 && tid < kChunk) wnan[buf][tid] = 0;
     __syncthreads();
     load_rows(ch + 2 * (int64_t)gridDim.x, pre[1]);
     // ---- B: features (sklearn_analyser.py:52-69 / file_processing.py:51-66)
     const int64_t nwin64 = n_rows - base;
     const int nwin = (int)(nwin64 < kChunk ? nwin64 : kChunk);
-    for (int i = tid; i < nwin * mfcc_n; i += 256) {
+    if constexpr (MN > 0 && MN * (kChunk / 4) <= 256) {
+      // thread (c, q): coefficient c of windows 4q .. 4q+3, sliding over the
+      // eight rows 4q .. 4q+7 they span (all loads issued at once); windows
+      // past nwin read rows past the clip (zero-filled): written, not used
+      const int c = tid % MN, q = tid / MN;
+      if (q < kChunk / 4 && VAD_FFN_DIAG != 1) {
+        float a[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] = rw_[(4 * q + k) * kMaxCoefs + c];
+        const bool m0 = !H3 || c < in_dim, m1 = !H3 || MN + c < in_dim, m2 = !H3 || 2 * MN + c < in_dim;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const Feat3 ft = feature_triple(a[k], a[k + 1], a[k + 2], a[k + 3], a[k + 4], mode);
+          float* xw = Xb + (4 * q + k) * kXStride;
+          if constexpr (H3) {
+            // mn is NaN exactly when the coefficient is flat (d2 with it)
+            const bool nan = (m0 || m2) && ft.mn != ft.mn;
+            if (nan) wnan[buf][4 * q + k] = 1;
+            xw[c] = m0 && !nan ? ft.mn : 0.f;
+            xw[MN + c] = m1 ? ft.d1 : 0.f;
+            xw[2 * MN + c] = m2 && !nan ? ft.d2 : 0.f;
+          } else {
+            xw[c] = ft.mn;
+            xw[MN + c] = ft.d1;
+            xw[2 * MN + c] = ft.d2;
+          }
+        }
+      }
+    } else
+    for (int i = tid; i < (VAD_FFN_DIAG == 1 ? 0 : nwin * mfcc_n); i += 256) {
       const int w = i / mfcc_n, c = i - w * mfcc_n;
       const float* r = rw_ + w * kMaxCoefs + c;
       const Feat3 ft = feature_triple(r[0], r[kMaxCoefs], r[2 * kMaxCoefs], r[3 * kMaxCoefs],
@@ -566,7 +613,9 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
           x0[s][q + 4] = hi4[q];
         }
       }
-      z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(fh, (const float*)fb, (const float*)fv, x0);
+      if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
+      else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(fh, (const float*)fb, (const float*)fv, x0);
+      if (wnan[buf][wl]) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
     } else {
       float x[KS0];
 #pragma unroll
