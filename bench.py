@@ -100,7 +100,7 @@ def main():
 
     from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers
     from vad_amd.pipeline import VadPipeline
-    from vad_amd.dist import gather_labels
+    from vad_amd.dist import LabelGather
 
     topo = TOPOLOGY_BL13 if args.ffn == "bl13" else TOPOLOGY_REF39
     layers = random_layers(topo, seed=3)
@@ -114,11 +114,13 @@ def main():
     ffn_plan = pipe.ffn.plan
     stream = torch.cuda.current_stream()
 
+    gather = LabelGather(F - 5, dev) if world > 1 else None
+
     def step():
         pipe.mfcc(audio, out=mfcc)                       # HIP MFCC kernel
         ffn_plan.window_labels(mfcc, out=labels)          # HIP features + MFMA FFN kernel
         if world > 1:
-            gather_labels(labels)                          # RCCL: decisions -> rank 0
+            gather(labels)                                 # RCCL: decisions -> rank 0
 
     for _ in range(args.warmup):
         step()

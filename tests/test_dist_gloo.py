@@ -28,6 +28,13 @@ def _worker(rank, world, port, q):
     out = gather_labels(labels)
     if rank == 0:
         q.put(torch.cat(out).tolist())
+    # fixed-size, preallocated form (bench.py's per-step gather), twice
+    from vad_amd.dist import LabelGather
+    g = LabelGather(4, torch.device("cpu"))
+    for step in range(2):
+        got = g(torch.full((4,), rank * 10 + step, dtype=torch.uint8))
+        if rank == 0:
+            q.put([t.tolist() for t in got])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -41,7 +48,10 @@ def test_gather_labels_gloo(world):
     for p in procs:
         p.start()
     got = q.get(timeout=120)
+    fixed = [q.get(timeout=120) for _ in range(2)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == [(i * 3) % 7 for i in range(11)]
+    for step, f in enumerate(fixed):
+        assert f == [[r * 10 + step] * 4 for r in range(world)]

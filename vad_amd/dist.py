@@ -22,7 +22,9 @@ def gather_labels(labels: torch.Tensor, dst=0, group=None):
     """Gather every rank's 1-D uint8 label tensor to `dst`.
 
     Returns the list of per-rank tensors on `dst` (None elsewhere).  Lengths
-    may differ per rank: sizes travel first, payloads are padded to the max.
+    may differ per rank: sizes travel first (a host sync), payloads are
+    padded to the max.  Steady-state callers with fixed sizes use
+    LabelGather, which allocates once and never syncs the host.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -34,11 +36,35 @@ def gather_labels(labels: torch.Tensor, dst=0, group=None):
     m = max(sizes) if sizes else 0
     buf = torch.zeros((m,), dtype=torch.uint8, device=dev)
     buf[:labels.numel()].copy_(labels.reshape(-1))
-    if dist.get_backend(group) == "nccl":
-        # RCCL gather = all_gather into rank-ordered slots (payload ~1 MB/rank)
-        out = [torch.empty_like(buf) for _ in range(world)]
-        dist.all_gather(out, buf, group=group)
-        return [o[:s] for o, s in zip(out, sizes)] if rank == dst else None
-    out = [torch.empty_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, out, dst=dst, group=group)
+    out = LabelGather(m, dev, dst, group)(buf)
     return [o[:s] for o, s in zip(out, sizes)] if rank == dst else None
+
+
+class LabelGather:
+    """Gather of a fixed-size uint8 label tensor from every rank to `dst`,
+    with the receive buffers allocated once: one collective per call, no
+    host synchronisation (the per-step form of bench.py).  With backend
+    "nccl" this is RCCL point-to-point (each rank sends its ~1 MB once, to
+    dst only, over its own xGMI link); should the backend refuse gather the
+    call falls back to all_gather into the same slots."""
+
+    def __init__(self, n, device, dst=0, group=None):
+        self.n, self.dst, self.group = int(n), dst, group
+        self.rank = dist.get_rank(group)
+        world = dist.get_world_size(group)
+        self.out = [torch.empty((self.n,), dtype=torch.uint8, device=device) for _ in range(world)]
+        self._use_gather = True
+
+    def __call__(self, labels: torch.Tensor):
+        if labels.numel() != self.n or labels.dtype != torch.uint8:
+            raise ValueError(f"expected {self.n} uint8 labels, got {labels.numel()} {labels.dtype}")
+        x = labels.reshape(-1)
+        if self._use_gather:
+            try:
+                dist.gather(x, self.out if self.rank == self.dst else None, dst=self.dst,
+                            group=self.group)
+                return self.out if self.rank == self.dst else None
+            except (RuntimeError, NotImplementedError):
+                self._use_gather = False
+        dist.all_gather(self.out, x, group=self.group)
+        return self.out if self.rank == self.dst else None
