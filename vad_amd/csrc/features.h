@@ -24,7 +24,8 @@ __device__ __forceinline__ Feat3 feature_triple(float a0, float a1, float a2, fl
     const float e0 = a0 - mean, e1 = a1 - mean, e2 = a2 - mean, e3 = a3 - mean, e4 = a4 - mean;
     const float var = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * 0.2f;
     const bool flat = (a0 == a1) & (a1 == a2) & (a2 == a3) & (a3 == a4);
-    mn = flat ? __builtin_nanf("") : e2 * rsqrtf(var);
+    // branch-free: the NaN is added in rather than selected around the rsqrt
+    mn = e2 * rsqrtf(var) + (flat ? __builtin_nanf("") : 0.f);
   }
   return {mn, a3 - a1, (a4 - mn) - (mn - a0)};
 }

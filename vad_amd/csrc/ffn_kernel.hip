@@ -472,10 +472,11 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 constexpr int kChunk = 64;
 constexpr int kXStride = 68;  // floats per feature row: 16-B aligned, conflict-free b128 reads
 
-template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN, bool H3>
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN, bool H3, int MODE = -1>
 __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* __restrict__ mfcc,
-                                                int64_t n_rows, int mfcc_n_rt, int mode,
+                                                int64_t n_rows, int mfcc_n_rt, int mode_rt,
                                                 uint8_t* __restrict__ labels) {
+  const int mode = MODE >= 0 ? MODE : mode_rt;  // compile-time feature form: no branches
   using TP = Topo<KS0, T1, T2, T3, T4, NC>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
   static_assert(!H3 || (MN > 0 && MN * (kChunk / 4) <= 256), "split-f16 needs the sliding feature phase");
@@ -517,14 +518,29 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
   // two chunks ahead
   constexpr int kRowRegs = ((kChunk + 4) * kMaxCoefs + 255) / 256;
   float pre[2][kRowRegs];
+  // MN > 0: rows packed at stride MN, so a chunk's rows are one contiguous
+  // run of (kChunk + 4) * MN floats copied element for element (branch-free:
+  // out-of-range lanes load element 0 and keep 0)
+  constexpr int kPackRegs = MN > 0 ? ((kChunk + 4) * MN + 255) / 256 : 1;
+  static_assert(MN == 0 || 256 * kPackRegs <= (kChunk + 4) * kMaxCoefs, "packed rows overflow");
   auto load_rows = [&](int64_t ch, float (&dst)[kRowRegs]) {
     const int64_t base = ch * kChunk;
     const int64_t avail = ch < n_chunks ? n_frames - base : 0;
     const int nr = (int)(avail < kChunk + 4 ? avail : kChunk + 4);
+    if constexpr (MN > 0) {
 #pragma unroll
-    for (int q = 0; q < kRowRegs; ++q) {
-      const int i = tid + 256 * q;
-      dst[q] = i < nr * mfcc_n ? mfcc[base * mfcc_n + i] : 0.f;
+      for (int q = 0; q < kPackRegs; ++q) {
+        const int i = tid + 256 * q;
+        const bool ok = i < nr * MN;
+        const float v = mfcc[ok ? base * MN + i : 0];
+        dst[q] = ok ? v : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < kRowRegs; ++q) {
+        const int i = tid + 256 * q;
+        dst[q] = i < nr * mfcc_n ? mfcc[base * mfcc_n + i] : 0.f;
+      }
     }
   };
   load_rows(blockIdx.x, pre[0]);
@@ -535,14 +551,22 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
     float* rw_ = rows[buf];
     float* Xb = X[buf];
     // ---- A: rows base .. base+67 (prefetched) ------------------------------
+    if constexpr (MN > 0) {
 #pragma unroll
-    for (int q = 0; q < kRowRegs; ++q) {
-      const int i = tid + 256 * q;
-      if (i < (kChunk + 4) * mfcc_n) {
-        const int r = i / mfcc_n, c = i - r * mfcc_n;
-        rw_[r * kMaxCoefs + c] = pre[0][q];
+      for (int q = 0; q < kPackRegs; ++q) {
+        rw_[tid + 256 * q] = pre[0][q];  // rows at stride MN (slots past the chunk unused)
+        pre[0][q] = pre[1][q];
       }
-      pre[0][q] = pre[1][q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < kRowRegs; ++q) {
+        const int i = tid + 256 * q;
+        if (i < (kChunk + 4) * mfcc_n) {
+          const int r = i / mfcc_n, c = i - r * mfcc_n;
+          rw_[r * kMaxCoefs + c] = pre[0][q];
+        }
+        pre[0][q] = pre[1][q];
+      }
     }
     if (H3 && tid < kChunk) wnan[buf][tid] = 0;
     __syncthreads();
@@ -558,19 +582,23 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
       if (q < kChunk / 4 && VAD_FFN_DIAG != 1) {
         float a[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] = rw_[(4 * q + k) * kMaxCoefs + c];
+        for (int k = 0; k < 8; ++k) a[k] = rw_[(4 * q + k) * MN + c];
         const bool m0 = !H3 || c < in_dim, m1 = !H3 || MN + c < in_dim, m2 = !H3 || 2 * MN + c < in_dim;
+        // feature groups no input of this topology can reach (in_dim <= 4 KS0)
+        constexpr bool kD1 = !H3 || MN < 4 * KS0, kD2 = !H3 || 2 * MN < 4 * KS0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const Feat3 ft = feature_triple(a[k], a[k + 1], a[k + 2], a[k + 3], a[k + 4], mode);
           float* xw = Xb + (4 * q + k) * kXStride;
           if constexpr (H3) {
-            // mn is NaN exactly when the coefficient is flat (d2 with it)
-            const bool nan = (m0 || m2) && ft.mn != ft.mn;
-            if (nan) wnan[buf][4 * q + k] = 1;
+            // mn is NaN exactly when the coefficient is flat (d2 with it);
+            // the flag is or-ed in by every coefficient thread, branch-free
+            const bool nan = (m0 || (kD2 && m2)) && ft.mn != ft.mn;
+            __hip_atomic_fetch_or(&wnan[buf][4 * q + k], (int)nan, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
             xw[c] = m0 && !nan ? ft.mn : 0.f;
-            xw[MN + c] = m1 ? ft.d1 : 0.f;
-            xw[2 * MN + c] = m2 && !nan ? ft.d2 : 0.f;
+            if constexpr (kD1) xw[MN + c] = m1 ? ft.d1 : 0.f;
+            if constexpr (kD2) xw[2 * MN + c] = m2 && !nan ? ft.d2 : 0.f;
           } else {
             xw[c] = ft.mn;
             xw[MN + c] = ft.d1;
@@ -581,9 +609,9 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
     } else
     for (int i = tid; i < (VAD_FFN_DIAG == 1 ? 0 : nwin * mfcc_n); i += 256) {
       const int w = i / mfcc_n, c = i - w * mfcc_n;
-      const float* r = rw_ + w * kMaxCoefs + c;
-      const Feat3 ft = feature_triple(r[0], r[kMaxCoefs], r[2 * kMaxCoefs], r[3 * kMaxCoefs],
-                                      r[4 * kMaxCoefs], mode);
+      constexpr int kRS = MN > 0 ? MN : kMaxCoefs;  // row stride of the staged rows
+      const float* r = rw_ + w * kRS + c;
+      const Feat3 ft = feature_triple(r[0], r[kRS], r[2 * kRS], r[3 * kRS], r[4 * kRS], mode);
       float* xw = Xb + w * kXStride;
       if constexpr (H3) {  // the split-f16 layer 0 reads every column: unused ones are 0
         xw[c] = c < in_dim ? ft.mn : 0.f;
@@ -636,12 +664,13 @@ __global__ __launch_bounds__(256) void ffn_window_kernel(FfnDev net, const float
   ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, false>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
 }
 
-// split-f16 variant: two 4-wave blocks per CU (<= 256 registers per lane)
-template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN>
+// split-f16 variant: two 4-wave blocks per CU (<= 256 registers per lane),
+// one instance per feature form
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MN, int MODE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffn_window_h3_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, int mfcc_n_rt, int mode,
     uint8_t* __restrict__ labels) {
-  ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, true>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
+  ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, true, MODE>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
 }
 
 // Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
@@ -752,8 +781,12 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
                          (KS0 == 4 && T1 == 4 && T2 == 4 && T3 == 1 && T4 == 0);
     if constexpr (kH3) {
       if (mfcc_n == 13 && net.fragh) {
-        hipLaunchKernelGGL((ffn_window_h3_kernel<KS0, T1, T2, T3, T4, NC, 13>), dim3((int)chunks),
-                           dim3(256), 0, st, net, in, n_rows, mfcc_n, mode, labels);
+        if (mode == VAD_FEAT_OFFLINE)
+          hipLaunchKernelGGL((ffn_window_h3_kernel<KS0, T1, T2, T3, T4, NC, 13, VAD_FEAT_OFFLINE>),
+                             dim3((int)chunks), dim3(256), 0, st, net, in, n_rows, mfcc_n, mode, labels);
+        else
+          hipLaunchKernelGGL((ffn_window_h3_kernel<KS0, T1, T2, T3, T4, NC, 13, VAD_FEAT_ANALYSER>),
+                             dim3((int)chunks), dim3(256), 0, st, net, in, n_rows, mfcc_n, mode, labels);
         return hipGetLastError();
       }
     }
