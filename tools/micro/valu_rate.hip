@@ -62,8 +62,13 @@ void run(const char* name, int threads) {
   const int per_iter = (KIND == 1) ? 32 : 16;
   const double instr = (double)iters * per_iter;       // per wave
   const int wps = threads / 256;                        // waves per SIMD
-  printf("%-14s waves/SIMD=%d  wall ns per wave-instr per SIMD=%.3f\n", name, wps,
-         best * 1e6 / (instr * wps));
+  unsigned long long hc[256 * 16];
+  (void)hipMemcpy(hc, cyc, sizeof(hc), hipMemcpyDeviceToHost);
+  // s_memtime ticks of wave 0 of block 0 over its loop: SIMD cycles per
+  // wave-instruction (all waves of the SIMD issuing) and the implied clock
+  const double cyc_per = (double)hc[0] / (instr * wps);
+  printf("%-14s waves/SIMD=%d  wall ns per wave-instr per SIMD=%.3f  cycles=%.2f  clock=%.2f GHz\n",
+         name, wps, best * 1e6 / (instr * wps), cyc_per, cyc_per / (best * 1e6 / (instr * wps)));
   (void)hipFree(out);
   (void)hipFree(cyc);
 }

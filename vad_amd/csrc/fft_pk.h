@@ -89,13 +89,18 @@ __device__ __forceinline__ v2f w16_5(v2f a) { return mul_cs<kmS16i, kC16i>(a); }
 __device__ __forceinline__ v2f w16_7(v2f a) { return mul_cs<kmC16i, kS16i>(a); }   // W16^7
 __device__ __forceinline__ v2f w8_1(v2f a) { return add_mi(a, a) * kC8; }          // W8^1 = W16^2
 
-// forward DFT4 (W4 = -i); y2, y3 given as x2 = (-i) y2, x3 = (-i) y3 when MI23
-template <bool MI23 = false>
+// forward DFT4 (W4 = -i); y2, y3 given as x2 = (-i) y2, x3 = (-i) y3 when MI23;
+// Z3: x3 is a known zero (the zero padding of the frame), so x1 +- x3 = x1
+// (the compiler may not fold x1 + 0: -0 + 0 = +0)
+template <bool MI23 = false, bool Z3 = false>
 __device__ __forceinline__ void dft4(v2f& x0, v2f& x1, v2f& x2, v2f& x3) {
   v2f t0, t1, t2, t3;
   if constexpr (MI23) {
     t0 = add_mi(x0, x2); t1 = sub_mi(x0, x2);
     t2 = add_mi(x1, x3); t3 = sub_mi(x1, x3);
+  } else if constexpr (Z3) {
+    t0 = x0 + x2; t1 = x0 - x2;
+    t2 = x1; t3 = x1;
   } else {
     t0 = x0 + x2; t1 = x0 - x2;
     t2 = x1 + x3; t3 = x1 - x3;
@@ -128,10 +133,12 @@ __device__ __forceinline__ void dft16(v2f (&x)[16]) {
 #pragma unroll
   for (int n = NZ; n < 16; ++n) x[n] = (v2f){0.f, 0.f};
   v2f v[4][4];
+  static_assert(NZ > 12, "the first-stage DFT4s assume x[0..12] may be non-zero");
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     v2f a0 = x[b], a1 = x[4 + b], a2 = x[8 + b], a3 = x[12 + b];
-    dft4(a0, a1, a2, a3);
+    if (12 + b >= NZ) dft4<false, true>(a0, a1, a2, a3);
+    else dft4(a0, a1, a2, a3);
     v[b][0] = a0; v[b][1] = a1; v[b][2] = a2; v[b][3] = a3;
   }
   // c = 0: no twiddles

@@ -35,8 +35,17 @@
 
 namespace vad {
 
-constexpr int kTile = 64;        // frames per workgroup tile
-constexpr int kThreads = 512;    // 8 waves
+// VAD_WG256: 256-thread workgroups of 32-frame tiles, two per CU (each
+// SIMD hosts one wave of each, so one workgroup's barrier waits and
+// phase 2 overlap the other's FFT); default: one 512-thread workgroup of
+// 64-frame tiles per CU
+#ifndef VAD_WG256
+#define VAD_WG256 0
+#endif
+constexpr int kTile = VAD_WG256 ? 32 : 64;        // frames per workgroup tile
+constexpr int kThreads = VAD_WG256 ? 256 : 512;   // 4 or 8 waves
+constexpr int kWaves = kThreads / 64;
+constexpr int kWgPerCu = VAD_WG256 ? 2 : 1;
 constexpr int kGroups = kThreads / 16;  // frames per phase-1 pass
 constexpr int kColStride = 18;   // complex per LDS column: 16-B aligned columns whose
                                  // ds_read_b128 lane groups hit disjoint banks
@@ -138,16 +147,18 @@ __device__ __forceinline__ void pad_stage_a(int len_rt, int n2, v2f (&u)[NU]) {
 //   column cO = 16 - cE (lanes 0..13 cover columns 1..7 / 9..15, lane 14
 //   column 0, lane 15 column 8); the pair m = (a_m, b_m) of the real-FFT
 //   split is (E[m], O[7-m]) = (Z[k], Z[256-k]) with k = cE + 32 m.
-//   Column 0 pairs k2 with -k2 (mod 16) instead, so lane 14 permutes its
-//   registers into (Z[16 m], Z[256 - 16 m]) pairs; its m = 0 pair holds the
-//   two self-partnered bins 0 and 128, fixed up explicitly.
+//   Column 0 pairs k2 with -k2 (mod 16) instead, i.e. E with E and O with
+//   O; lane 14 keeps whichever half of the regular pair already matches:
+//   m = 1..3 (E[m], E[8-m]), m = 4..7 (O[m], O[7-m]), so it needs one
+//   select per pair, not two; its m = 0 pair (E[0], E[4]) holds the two
+//   self-partnered bins 0 and 128, fixed up explicitly.
 struct LaneConsts {
   v2f twa[16];     // W256^(j k1)
   v2f twb[8];      // W512^kE(m)
   int cE, cO;
-  int e0, es;      // kE(m) = e0 + es*m
-  int o0;          // kO(m) = o0 - es*m (m >= 1)
-  int kO0;         // kO(0)
+  int e0;          // kE(m) = e0 + 32 m (+ off4 for m >= 4)
+  int off4;        // 16 on the column-0 lane (its m >= 4 pairs are odd bins), else 0
+  int kO0;         // kO(0); kO(m >= 1) = 256 - kE(m)
   bool col0;
 };
 
@@ -161,15 +172,14 @@ __device__ __forceinline__ void lane_consts(const MfccDev* __restrict__ plan, in
   }
   L.col0 = (j == 14);
   L.e0 = L.cE;
-  L.es = L.col0 ? 16 : 32;
-  L.o0 = 256 - L.cE;
+  L.off4 = L.col0 ? 16 : 0;
   L.kO0 = L.col0 ? 128 : 256 - L.cE;
   const v2f* ta = reinterpret_cast<const v2f*>(plan->tw_a);
   const v2f* tb = reinterpret_cast<const v2f*>(plan->tw_b);
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) L.twa[k1] = ta[j * 16 + k1];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) L.twb[m] = tb[L.e0 + L.es * m];
+  for (int m = 0; m < 8; ++m) L.twb[m] = tb[L.e0 + 32 * m + (m >= 4 ? L.off4 : 0)];
 }
 
 // Phase 1 for one frame of a 16-lane group, in three steps so that a wave
@@ -257,13 +267,13 @@ __device__ __forceinline__ void finish_b(const LaneConsts& L, v2f (&col)[32],
   //   2 X[k] = S - i W^k D,  2 X[256-k] = conj(S) - i conj(W^k D),
   //   S = a + conj(b), D = a - conj(b),  W = W512
   //   U = (Re 2X[k], Re 2X[256-k]), V = (Im 2X[k], Im 2X[256-k])
-  // column-0 lane: E' = (Z0, Z16, ..., Z112), O'[7-m] = Z[256 - 16 m]
-  const v2f Ep[8] = {E[0], O[0], E[1], O[1], E[2], O[2], E[3], O[3]};
-  const v2f Op[8] = {O[4], E[5], O[5], E[6], O[6], E[7], O[7], E[4]};
+  // column-0 lane: (E[0], E[4]) = (Z0, Z128); (E[m], E[8-m]) = (Z[32 m],
+  // Z[256 - 32 m]) for m = 1..3; (O[m], O[7-m]) = (Z[32 m + 16],
+  // Z[240 - 32 m]) for m = 4..7
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
-    const v2f a = L.col0 ? Ep[m] : E[m];
-    const v2f b = L.col0 ? Op[7 - m] : O[7 - m];
+    const v2f a = (m >= 4 && L.col0) ? O[m] : E[m];
+    const v2f b = (m < 4 && L.col0) ? E[m == 0 ? 4 : (8 - m) & 7] : O[7 - m];
     const v2f S = pk::add_conj(a, b);
     const v2f T = pk::cmul(pk::sub_conj(a, b), L.twb[m]);
     const v2f U = pk::split_u(S, T);
@@ -278,8 +288,8 @@ __device__ __forceinline__ void finish_b(const LaneConsts& L, v2f (&col)[32],
       pk = L.col0 ? p0 : pk;
       pn = L.col0 ? p128 : pn;
     }
-    const int kE = L.e0 + L.es * m;
-    const int kO = m == 0 ? L.kO0 : L.o0 - L.es * m;
+    const int kE = L.e0 + 32 * m + (m >= 4 ? L.off4 : 0);
+    const int kO = m == 0 ? L.kO0 : 256 - kE;
     prow[kE] = pk;
     prow[kO] = pn;
   }
@@ -299,7 +309,24 @@ __device__ __forceinline__ float log10_pos(float e) {
 template <int SPEC>
 constexpr int lm_stride() { return SPEC == 1 ? 28 : SPEC == 2 ? 44 : kMaxFilters + 4; }
 constexpr int kLmFloats = kTile * (kMaxFilters + 4);
-constexpr int kDctGroups = 4;  // phase 2b: waves 0..3, coefficients c = w, w+4, w+8, w+12
+// Phase 2b coefficient groups: VAD_DCT8 = 0: waves 0..3 own c = w, w+4, w+8,
+// w+12; VAD_DCT8 = 1: every wave owns c = w, w+8.
+#ifndef VAD_DCT8
+#define VAD_DCT8 0
+#endif
+constexpr int kDctGroups = VAD_DCT8 ? 8 : 4;
+constexpr int kDctPer = 16 / kDctGroups;  // coefficients per group (mfcc_n <= 16)
+// VAD_PRIO = k > 0 (paired-frame loop): waves 4..7 (the arbitration losers,
+// MI355X_MICROARCH.md "Two waves per SIMD") run the first k segments of each
+// tile's FFT at s_setprio 1, the rest at 0, so that both waves of a SIMD
+// finish phase 1 together instead of the younger finishing alone.
+#ifndef VAD_PRIO
+#define VAD_PRIO 0
+#endif
+#ifndef VAD_LATE_BAR2
+#define VAD_LATE_BAR2 0
+#endif
+constexpr bool kLateBar2 = VAD_LATE_BAR2 != 0;
 
 // Phase 2a (runtime plan): frame `lane`, filters [fb, fe) -> log-mel row.
 __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
@@ -329,10 +356,10 @@ __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
 // coefficients c = g + 4 i of group g.
 __device__ __forceinline__ void dct_rt(const MfccDev* __restrict__ plan,
                                        const float* __restrict__ lrow, int g, int mfcc_n,
-                                       float (&acc)[4]) {
+                                       float (&acc)[kDctPer]) {
   const int nf = plan->n_filters;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < kDctPer; ++i) {
     const int c = g + kDctGroups * i;
     float s0 = 0.f, s1 = 0.f;
     if (c < mfcc_n) {
@@ -359,6 +386,8 @@ __device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
                                               float* __restrict__ lm);
 template <class T, int G>
 __device__ __forceinline__ void dct_code(const float* __restrict__ lm, float (&acc)[4]);
+template <class T, int G>
+__device__ __forceinline__ void dct8_code(const float* __restrict__ lm, float (&acc)[2]);
 
 #include "mel_code.h"
 
@@ -378,13 +407,26 @@ __device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float*
 }
 
 template <class T>
-__device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&acc)[4]) {
+__device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&acc)[kDctPer]) {
   lrow = static_cast<const float*>(__builtin_assume_aligned(lrow, 16));
-  switch (g) {
-    case 0: dct_code<T, 0>(lrow, acc); break;
-    case 1: dct_code<T, 1>(lrow, acc); break;
-    case 2: dct_code<T, 2>(lrow, acc); break;
-    default: dct_code<T, 3>(lrow, acc); break;
+  if constexpr (kDctGroups == 8) {
+    switch (g) {
+      case 0: dct8_code<T, 0>(lrow, acc); break;
+      case 1: dct8_code<T, 1>(lrow, acc); break;
+      case 2: dct8_code<T, 2>(lrow, acc); break;
+      case 3: dct8_code<T, 3>(lrow, acc); break;
+      case 4: dct8_code<T, 4>(lrow, acc); break;
+      case 5: dct8_code<T, 5>(lrow, acc); break;
+      case 6: dct8_code<T, 6>(lrow, acc); break;
+      default: dct8_code<T, 7>(lrow, acc); break;
+    }
+  } else {
+    switch (g) {
+      case 0: dct_code<T, 0>(lrow, acc); break;
+      case 1: dct_code<T, 1>(lrow, acc); break;
+      case 2: dct_code<T, 2>(lrow, acc); break;
+      default: dct_code<T, 3>(lrow, acc); break;
+    }
   }
 }
 
@@ -395,9 +437,23 @@ __device__ __forceinline__ void phase2a(const MfccDev* __restrict__ plan, const 
                                         float* lm, int wave, int lane) {
   const float* prow = P + lane * kPStride;
   float* lrow = lm + lane * lm_stride<SPEC>();
-  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
-  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
-  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
+  if constexpr (kWaves == 8) {
+    if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
+    else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
+    else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
+  } else {  // 4 waves, 32-frame tiles: wave w runs bands 2w and 2w + 1 on lanes 0..31
+    if (lane < kTile) {
+      if constexpr (SPEC == 1) {
+        mel_dispatch<Mel26>(2 * wave, prow, lrow);
+        mel_dispatch<Mel26>(2 * wave + 1, prow, lrow);
+      } else if constexpr (SPEC == 2) {
+        mel_dispatch<Mel40>(2 * wave, prow, lrow);
+        mel_dispatch<Mel40>(2 * wave + 1, prow, lrow);
+      } else {
+        mel_log(plan, prow, plan->wave_fbeg[2 * wave], plan->wave_fend[2 * wave + 1], lrow);
+      }
+    }
+  }
 }
 
 // Phase 2b (waves 0..3): lifter x DCT of the tile's log-mel rows, one frame
@@ -408,8 +464,9 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
                                         int mfcc_n_rt, float* __restrict__ out) {
   constexpr int NC = SPEC == 1 ? Mel26::NC : SPEC == 2 ? Mel40::NC : 0;
   const int mfcc_n = NC > 0 ? NC : mfcc_n_rt;
+  if (kTile < 64 && lane >= kTile) return;
   const float* lrow = lm + lane * lm_stride<SPEC>();
-  float acc[4];
+  float acc[kDctPer];
   if constexpr (SPEC == 1) dct_dispatch<Mel26>(wave, lrow, acc);
   else if constexpr (SPEC == 2) dct_dispatch<Mel40>(wave, lrow, acc);
   else dct_rt(plan, lrow, wave, mfcc_n, acc);
@@ -418,11 +475,14 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
     if (f < n_frames) {
       float* o = out + f * mfcc_n;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < kDctPer; ++i)
         if (wave + kDctGroups * i < mfcc_n) o[wave + kDctGroups * i] = acc[i];
     }
   } else {
-    if (acc[0] == 12345.f) out[0] = acc[1] + acc[2] + acc[3];  // keep the work live
+    float t = 0.f;
+#pragma unroll
+    for (int i = 1; i < kDctPer; ++i) t += acc[i];
+    if (acc[0] == 12345.f) out[0] = t;  // keep the work live
   }
 }
 
@@ -434,7 +494,7 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
 // time the older waves' phases alone.
 #define VAD_STAMP(k)                                                              \
   do {                                                                            \
-    if constexpr (DIAG >= 5) {                                                    \
+    if constexpr (DIAG == 5 || DIAG == 6) {                                       \
       __builtin_amdgcn_sched_barrier(0);                                          \
       st_[k] = __builtin_amdgcn_s_memtime();                                      \
       __builtin_amdgcn_sched_barrier(0);                                          \
@@ -462,7 +522,7 @@ __device__ __forceinline__ void lds_barrier() {
 // DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
 // HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0>
-__global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
+__global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -513,9 +573,9 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
       return src + (F < flast ? F : flast) * frame_stride;
     };
-    const int64_t per = (n_tiles + gridDim.x - 1) / gridDim.x;
-    const int64_t t_end = ((int64_t)blockIdx.x + 1) * per < n_tiles ? ((int64_t)blockIdx.x + 1) * per : n_tiles;
-    int64_t tile = (int64_t)blockIdx.x * per;
+    // contiguous, balanced runs: workgroup b owns tiles [b T / G, (b + 1) T / G)
+    int64_t tile = (int64_t)blockIdx.x * n_tiles / gridDim.x;
+    const int64_t t_end = ((int64_t)blockIdx.x + 1) * n_tiles / gridDim.x;
     v2f buf[NB];
     {
       int lim;
@@ -523,6 +583,16 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
     }
     __builtin_amdgcn_sched_barrier(0);
+    // DIAG 9: per-workgroup start / end (s_memtime, s_memrealtime) after the
+    // MFCC rows, in a buffer the caller over-allocates; outputs stay exact
+    unsigned long long* wg_st = reinterpret_cast<unsigned long long*>(out + n_frames * 13) + blockIdx.x * 4;
+    (void)wg_st;
+    if constexpr (DIAG == 9) {
+      if (tid == 0) {
+        wg_st[0] = __builtin_amdgcn_s_memtime();
+        wg_st[1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
     int64_t prev_f0 = -1;
     unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
     (void)stamps;
@@ -544,8 +614,23 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       int lim;
       const TIN* nb = pair_base(tile + 1, lim);
       v2f u[16], col[32];
+      // VAD_PRIO: the younger half leads the first VAD_PRIO segments
+#define VAD_PRIO_AT(k)                                                  \
+  do {                                                                  \
+    if constexpr (VAD_PRIO == (k)) {                                    \
+      __builtin_amdgcn_sched_barrier(0);                                \
+      if (wave >= 4) __builtin_amdgcn_s_setprio((k) == 0 ? 1 : 0);      \
+      __builtin_amdgcn_sched_barrier(0);                                \
+    }                                                                   \
+  } while (0)
+      if constexpr (VAD_PRIO > 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       VAD_STAMP(0);
       stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+      VAD_PRIO_AT(1);
       VAD_STAMP(1);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
@@ -553,36 +638,46 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       store_a(u, gscr, j);
       read_b(L, gscr, col);
       __builtin_amdgcn_sched_barrier(0);
+      VAD_PRIO_AT(2);
       VAD_STAMP(2);
       // pass 1's stage A covers the latency of pass 0's transpose reads
       stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
+      VAD_PRIO_AT(3);
+      // VAD_LATE_BAR2: the previous tile's phase 2a must have read P before
+      // this tile's first power row lands; waiting here, not right after
+      // phase 2a, lets a wave run into this tile's stage A meanwhile
+      if constexpr (kLateBar2 && MODE == kAudioToMfcc && DIAG != 10)
+        if (prev_f0 >= 0) lds_barrier();
       VAD_STAMP(3);
       if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
+      VAD_PRIO_AT(4);
       VAD_STAMP(4);
       store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
       read_b(L, gscr, col);
+      VAD_PRIO_AT(5);
       VAD_STAMP(5);
       if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
-      if constexpr (MODE == kAudioToMfcc) {
+      VAD_PRIO_AT(6);
+      if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(6);
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
         phase2a<SPEC>(plan, P, lm, wave, lane);
         VAD_STAMP(9);
-        lds_barrier();  // log-mel rows complete; P and the FFT scratch free
+        if constexpr (!kLateBar2) lds_barrier();  // log-mel rows complete; P and the FFT scratch free
         VAD_STAMP(10);
         prev_f0 = f0;
-        if constexpr (DIAG >= 5) {
+        if constexpr (DIAG == 5 || DIAG == 6) {
           if (lane == 0 && it < 8) {
 #pragma unroll
             for (int k = 0; k < kStamps; ++k)
@@ -592,8 +687,16 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       }
     }
     if constexpr (MODE == kAudioToMfcc) {
+      if constexpr (kLateBar2 && DIAG != 10) lds_barrier();  // the last log-mel rows complete
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+    }
+    if constexpr (DIAG == 9) {
+      __syncthreads();
+      if (tid == 0) {
+        wg_st[2] = __builtin_amdgcn_s_memtime();
+        wg_st[3] = __builtin_amdgcn_s_memrealtime();
+      }
     }
   } else {
     v2f* gscr = scr + grp * kGroupScratch;
@@ -614,9 +717,9 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     };
     // each workgroup owns a contiguous run of tiles: consecutive tiles are
     // adjacent in memory (shared halo in this XCD's L2, page-local loads)
-    const int64_t per = (n_tiles + gridDim.x - 1) / gridDim.x;
-    const int64_t t_end = ((int64_t)blockIdx.x + 1) * per < n_tiles ? ((int64_t)blockIdx.x + 1) * per : n_tiles;
-    int64_t tile = (int64_t)blockIdx.x * per;
+    // contiguous, balanced runs: workgroup b owns tiles [b T / G, (b + 1) T / G)
+    int64_t tile = (int64_t)blockIdx.x * n_tiles / gridDim.x;
+    const int64_t t_end = ((int64_t)blockIdx.x + 1) * n_tiles / gridDim.x;
     // issue order = the steady state's (pass 0 then pass 1): the waitcnt
     // pass merges the prologue into the loop header, and an interleaved
     // prologue would make the first stage A wait for every load in flight
@@ -651,7 +754,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       const bool work = DIAG != 6 || wave < 4;
       VAD_STAMP(0);
       v2f u[16], col[32];
-      if (work && LEN > 0 && kSplitLoads && DIAG < 5) {
+      if (work && LEN > 0 && kSplitLoads && DIAG != 5 && DIAG != 6) {
         // the next tile's sample loads go out in chunks spread over the
         // tile: a wave's 13 back-to-back pair loads (x 8 waves) would fill
         // the texture address queue and hold every wave at its load burst
@@ -722,7 +825,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // first (waves 0..3 are older and win VALU arbitration on their
         // SIMD) while their SIMD partners are still in their FFT
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -731,7 +834,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         lds_barrier();  // log-mel rows complete; P and the FFT scratch free
         VAD_STAMP(10);
         prev_f0 = f0;
-        if constexpr (DIAG >= 5) {
+        if constexpr (DIAG == 5 || DIAG == 6) {
           if (lane == 0 && it < 8) {
 #pragma unroll
             for (int k = 0; k < kStamps; ++k)
@@ -742,7 +845,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     }
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG < 5 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -765,7 +868,7 @@ template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, 
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int cap = num_cus();  // persistent: one 512-thread workgroup per CU (LDS-bound)
+  const int cap = num_cus() * kWgPerCu;  // persistent, LDS-bound: kWgPerCu workgroups per CU
   const int grid = (int)(n_tiles < cap ? n_tiles : cap);
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;
@@ -792,6 +895,10 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
       static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
       if (diag == 5 && stride == 160 && kPairFrames)
         return launch_t<TIN, MODE, 13, true, 400, 1, 5, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 9 && stride == 160 && kPairFrames)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 9, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 10 && stride == 160 && kPairFrames)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 10, 5>(plan, src, stride, len, n, out, st);
       if (diag == 5 || diag == 8) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
       if (diag == 6) return launch_t<TIN, MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
       if (diag == 7) return launch_t<TIN, MODE, 13, true, 400, 1, 7>(plan, src, stride, len, n, out, st);

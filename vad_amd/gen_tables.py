@@ -28,7 +28,6 @@ CONFIGS = [
 ]
 WAVES = 8          # phase-2a filter bands (one per wave)
 DCT_GROUPS = 4     # phase-2b coefficient groups c = g, g+4, ... (waves 0..3)
-DCT_PER_GROUP = 4
 
 
 def mel_filterbank(lo, hi, nf, sr, fft_n=512):
@@ -166,11 +165,24 @@ def emit_code(name, info):
                        f"  // (==0 -> eps), log10")
         out.append("}")
         out.append("")
+    for ng, fname in ((DCT_GROUPS, "dct_code"), (8, "dct8_code")):
+        out += dct_groups(name, d, ng, fname)
+    return "\n".join(out)
+
+
+def dct_groups(name, d, ng, fname):
+    """lifter x DCT of a log-mel row for the coefficient groups c = g + ng i
+    (ng = 4: waves 0..3 own four coefficients each; ng = 8: every wave owns
+    one or two)."""
+    nf, nc = d.shape[1], d.shape[0]
+    per = (nc + ng - 1) // ng
+    comp = "xyzw"
+    out = []
     nq = (nf + 3) // 4
-    for g in range(DCT_GROUPS):
-        coefs = list(range(g, nc, DCT_GROUPS))
-        out.append(f"template <> __device__ __forceinline__ void dct_code<{name}, {g}>(")
-        out.append(f"    const float* __restrict__ lm, float (&acc)[{DCT_PER_GROUP}]) {{")
+    for g in range(ng):
+        coefs = list(range(g, nc, ng))
+        out.append(f"template <> __device__ __forceinline__ void {fname}<{name}, {g}>(")
+        out.append(f"    const float* __restrict__ lm, float (&acc)[{per}]) {{")
         for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
                        f"__builtin_assume_aligned(lm + {4 * q}, 16));")
@@ -188,11 +200,11 @@ def emit_code(name, info):
                 op = "v_mul_f32_e32" if step == 0 else "v_fmac_f32_e32"
                 cons = "=v" if step == 0 else "+v"
                 out.append(f'  asm volatile("{op} %0, {bits(d[c, m])}, %1" : "{cons}"({reg}) : "v"({src}));')
-        for i in range(DCT_PER_GROUP):
+        for i in range(per):
             out.append(f"  acc[{i}] = a{i} + b{i};" if i < len(coefs) else f"  acc[{i}] = 0.f;")
         out.append("}")
         out.append("")
-    return "\n".join(out)
+    return out
 
 
 def main():
