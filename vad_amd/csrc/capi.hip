@@ -271,8 +271,10 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   std::vector<uint32_t> fragh;
   const bool use_h3 = (ref39 || bl13) && !getenv("VAD_FFN_EXACT");
   if (use_h3) {
-    const int hl = bl13 ? n_layers - 1 : n_layers;  // bl13's output layer stays on the VALU
-    for (int l = 0; l < hl; ++l) {
+    // every layer, output included: the block kernel runs bl13's output
+    // layer on the VALU and reads only the hidden layers' slots (the first
+    // ones); the wave kernel runs all of them on the MFMA
+    for (int l = 0; l < n_layers; ++l) {
       const int ks = l == 0 ? (dims[0] + 31) / 32 : (tiles[l - 1] + 1) / 2;
       for (int mt = 0; mt < tiles[l]; ++mt)
         for (int s = 0; s < ks; ++s)

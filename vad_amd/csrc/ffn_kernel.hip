@@ -89,12 +89,13 @@ __device__ __forceinline__ void dense_layer(const float* __restrict__ a, const f
 // classes the argmax reads (<= 4).  VL: the output layer runs on the VALU
 // when its input spans >= 2 tiles -- a 16-row MFMA tile would waste 16-NC of
 // its rows (13-64-64-2: 16 MFMAs per 16 windows become 32 FMAs per lane and a
-// cross-lane sum).
-template <int KS0, int T1, int T2, int T3, int T4, int NC = 4>
+// cross-lane sum).  NOVL keeps the output layer on the MFMA regardless (the
+// wave kernel's split-f16 form, where it is the cheaper of the two).
+template <int KS0, int T1, int T2, int T3, int T4, int NC = 4, bool NOVL = false>
 struct Topo {
   static constexpr int NL = (T1 > 0) + (T2 > 0) + (T3 > 0) + (T4 > 0);
   static constexpr int TIL = NL == 2 ? T1 : NL == 3 ? T2 : NL == 4 ? T3 : 0;  // last layer's input tiles
-  static constexpr bool VL = NL >= 2 && TIL >= 2;
+  static constexpr bool VL = !NOVL && NL >= 2 && TIL >= 2;
   static constexpr int A0 = T1 * KS0;
   static constexpr int A1 = T2 * T1 * 4;
   static constexpr int A2 = T3 * T2 * 4;
@@ -135,6 +136,33 @@ __device__ __forceinline__ void load_frags(const float* __restrict__ frag, int l
   fv[TP::NV + TP::NVB] = 0.f;
 }
 
+// Cross-row sums on the gfx950 row-swap permutes (VALU, no LDS round trip
+// like ds_bpermute): v_permlane16_swap exchanges rows 1 / 3 of its first
+// operand with rows 0 / 2 of its second, so with both holding p the two
+// results add to p + p[lane ^ 16]; v_permlane32_swap likewise gives
+// p + p[lane ^ 32].  Each lane's sum takes its operands in the same order as
+// p + __shfl_xor(p, 16) then + __shfl_xor(., 32) (fp add commutes: results
+// identical).  Inline asm: the clang builtin returns the first operand twice
+// (checked on the device, tools/micro/permlane_check.hip); the s_nops cover
+// the VALU-write -> permlane-read and permlane-write -> VALU-read distances
+// the compiler cannot see through asm.
+__device__ __forceinline__ float lane_sum_xor48(float p) {
+  float a = p, b = p;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  float s = a + b;
+  float c = s, d = s;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
+  return c + d;
+}
+__device__ __forceinline__ int lane_or_xor48(int v) {
+  int a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  int o = a | b;
+  int c = o, d = o;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
+  return c | d;
+}
+
 // VALU output layer: lane (g, window jw) holds hidden units 16t + 4g + r of
 // its window; each class is a 16-term partial sum per lane, completed across
 // the four lane groups (xor 16, xor 32: a fixed association, deterministic).
@@ -153,9 +181,7 @@ __device__ __forceinline__ f32x4 valu_out_layer(FV fv, const f32x4 (&h)[TI], flo
         p1 = fmaf(fv[(c * TI + t) * 4 + r + 1], h[t][r + 1], p1);
       }
     }
-    float p = p0 + p1;
-    p += __shfl_xor(p, 16);
-    p += __shfl_xor(p, 32);
+    const float p = lane_sum_xor48(p0 + p1);
     z[c] = p + fv[TP::NV + c] * bias_scale;
   }
   return z;
@@ -233,9 +259,15 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
   for (int q = 0; q < 8; q += 2) {
     const f2 p = {v[q], v[q + 1]};
     const h2 h = __builtin_convertvector(p, h2);
-    const h2 r = __builtin_convertvector(p - __builtin_convertvector(h, f2), h2);
-    hw[q / 2] = __builtin_bit_cast(unsigned, h);
-    lw[q / 2] = __builtin_bit_cast(unsigned, r);
+    // lo = f16(v - f32(hi)) per half, one mixed-precision fma each (f16
+    // source, f32 addend, one rounding to f16): the same bits as converting
+    // hi back, subtracting in f32 (exact) and converting the difference
+    unsigned l;
+    const unsigned hb = __builtin_bit_cast(unsigned, h);
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hb), "v"(v[q]));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hb), "v"(v[q + 1]));
+    hw[q / 2] = hb;
+    lw[q / 2] = l;
   }
   hi = __builtin_bit_cast(h8, hw);
   lo = __builtin_bit_cast(h8, lw);
@@ -376,10 +408,11 @@ __device__ __forceinline__ const u4 (&frag_slice(const u4 (&fh)[M][2]))[N][2] {
 
 // Forward of one 16-window tile: x0 holds the layer-0 inputs of K-step s,
 // k = 8g + q (g = lane >> 4).
-template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV>
-__device__ __forceinline__ f32x4 mlp_forward_h3(const u4 (&fh)[HTopo<Topo<KS0, T1, T2, T3, T4, NC>, KS0, T1, T2, T3, T4>::NS][2],
-                                                FB fb, FV fv, float (&x0)[(4 * KS0 + 31) / 32][8]) {
-  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
+template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV, bool NOVL = false>
+__device__ __forceinline__ f32x4 mlp_forward_h3(
+    const u4 (&fh)[HTopo<Topo<KS0, T1, T2, T3, T4, NC, NOVL>, KS0, T1, T2, T3, T4>::NS][2], FB fb, FV fv,
+    float (&x0)[(4 * KS0 + 31) / 32][8]) {
+  using TP = Topo<KS0, T1, T2, T3, T4, NC, NOVL>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
   f32x4 h1[T1];
   dense_h3<T1, HP::K0, FB>(frag_slice<HP::S0, 0>(fh), fb, x0, h1, TP::NL > 1);
@@ -673,6 +706,149 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
   ffn_window_body<KS0, T1, T2, T3, T4, NC, MN, true, MODE>(net, mfcc, n_rows, mfcc_n_rt, mode, labels);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-autonomous window kernel (split-f16 topologies, 13 coefficients).
+// Each wave owns whole 16-window tiles end to end: the tile's 20 MFCC rows
+// (16 windows + 4 halo rows, one contiguous run of 260 floats) are loaded
+// into registers one tile ahead, staged in a wave-private LDS slice, turned
+// into the tile's 16 x 13 feature triples (3.25 per lane; item i reads
+// R[i + 13 d], conflict-free) in a second wave-private slice, read back as
+// the layer-0 B operands and classified.  No workgroup barriers: the waves of
+// a SIMD drift freely, so one wave's LDS / MFMA latency hides behind the
+// other's VALU work (the 64-window block kernel above pays two barriers and
+// a block-wide load -> features -> MLP chain per chunk).
+//   NaN windows (a flat coefficient, the analyser's 0/0): the feature item
+// writes 0 and flags its window; the window's logits become NaN -> class 0,
+// as in ffn_window_body.
+// ---------------------------------------------------------------------------
+#ifndef VAD_FFN_WAVE
+#define VAD_FFN_WAVE 1  // 0: the 64-window block kernel for the split-f16 topologies
+#endif
+#ifndef VAD_FFN_WAVE_MFMA_OUT
+#define VAD_FFN_WAVE_MFMA_OUT 0
+#endif
+constexpr int kWTile = 16;                       // windows per wave tile
+constexpr int kWRows = (kWTile + 4) * 13;        // staged MFCC floats per tile (260)
+constexpr int kWRowRegs = (kWRows + 63) / 64;    // 5 per lane
+
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffn_wave_kernel(
+    FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
+  // VAD_FFN_WAVE_MFMA_OUT: the output layer on the MFMA too (the plan's
+  // fragh holds its slots after the hidden layers'); default: bl13's on the
+  // VALU (its 6-MFMA single-tile chain measured 3 us slower per 1M windows)
+  using TP = Topo<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0>;
+  using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+  constexpr int MN = 13;
+  static_assert(KS0 == 4 || KS0 == 10, "specialised topologies: 13 or 39 inputs");
+  constexpr int IN = KS0 == 4 ? MN : 3 * MN;  // network inputs (features 0 .. IN-1)
+  constexpr int XS = 32 * HP::K0 + 4;         // floats per feature row: 16-B aligned
+  __shared__ float rows_s[4][kWRows];
+  __shared__ __attribute__((aligned(16))) float x_s[4][kWTile * XS];
+  __shared__ int flat_s[4][kWTile];  // per window: some coefficient is flat (NaN features)
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+  const int g = lane >> 4;
+  const int jw = lane & 15;
+  float* R = rows_s[wv];
+  float* X = x_s[wv];
+  int* FL = flat_s[wv];
+
+  float fa[1];
+  float fb[TP::NB];
+  float fv[TP::NV + TP::NVB + 1];
+  u4 fh[HP::NS][2];
+  load_frags<TP, true>(net.frag, lane, fa, fb, fv);
+  load_fragh<HP>(net.fragh, lane, fh);
+  // feature columns IN .. 32 K0 - 1 are read by layer 0 and stay 0
+  for (int i = lane; i < kWTile * XS; i += 64) X[i] = 0.f;
+
+  const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
+  const int64_t total = (n_rows + 4) * MN;  // MFCC floats the windows can read
+  const int64_t wave_id = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * 4;
+  // branch-free and select-free (a select on the loaded value would make the
+  // prefetch wait at the loop's back edge): offsets past the rows clamp to
+  // the last float, so the last tile's unused windows see finite rows.  The
+  // tile base is wave-uniform (a scalar address), the lane offsets 32-bit.
+  auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
+    const int64_t base = t * (kWTile * MN);
+    const float* tb = mfcc + base;
+    const int64_t rem = total - 1 - base;  // >= 0 for t < n_tiles
+    const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);  // byte offset clamp
+#pragma unroll
+    for (int q = 0; q < kWRowRegs; ++q) {
+      const unsigned ob = 4u * (unsigned)(lane + 64 * q);
+      dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
+    }
+  };
+  // every fragment load done before the loop: the waitcnt pass would
+  // otherwise leave counter waits for them in the loop body, where they
+  // also wait on the row prefetches
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0
+  // one tile: rows (prefetched two tiles ahead in `pre`) -> R; pre reloaded
+  // with tile tn's rows; features -> X; MLP; label
+  auto tile_body = [&](int64_t t, int64_t tn, float (&pre)[kWRowRegs]) {
+#pragma unroll
+    for (int q = 0; q < kWRowRegs; ++q)
+      if (lane + 64 * q < kWRows) R[lane + 64 * q] = pre[q];
+    load(tn < n_tiles ? tn : t, pre);
+    // features (sklearn_analyser.py:52-69 / file_processing.py:51-66): item
+    // i = 13 w + c is coefficient c of window w; its rows are R[i + 13 d].
+    // A flat coefficient (the analyser's 0/0: mn and d2 NaN) writes its
+    // features as 0 and raises its window's flag -- plain stores of 1, after
+    // the wave's own zeroing stores in LDS order, so no atomics
+    if (lane < kWTile) FL[lane] = 0;
+#pragma unroll
+    for (int r = 0; r < (kWTile * MN + 63) / 64; ++r) {
+      const int it = lane + 64 * r;
+      if ((r < kWTile * MN / 64 || it < kWTile * MN) && VAD_FFN_DIAG != 1) {
+        const int w = it / MN, c = it - MN * w;
+        const Feat3 ft = feature_triple(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
+                                        R[it + 4 * MN], MODE);
+        const bool flat = ft.mn != ft.mn;
+        if (flat) FL[w] = 1;
+        float* xw = X + w * XS;
+        xw[c] = flat ? 0.f : ft.mn;
+        if constexpr (IN > MN) {
+          xw[MN + c] = ft.d1;
+          xw[2 * MN + c] = flat ? 0.f : ft.d2;
+        }
+      }
+    }
+    // layer-0 B operands: lane (g, jw) holds features 32 s + 8 g + q of window jw
+    float x0[HP::K0][8];
+    const v4f* xr = reinterpret_cast<const v4f*>(X + jw * XS + 8 * g);
+#pragma unroll
+    for (int s = 0; s < HP::K0; ++s) {
+      const v4f lo4 = xr[8 * s], hi4 = xr[8 * s + 1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        x0[s][q] = lo4[q];
+        x0[s][q + 4] = hi4[q];
+      }
+    }
+    const int wnan = FL[jw];
+    f32x4 z;
+    if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
+    else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, const float*, const float*, VAD_FFN_WAVE_MFMA_OUT != 0>(
+        fh, (const float*)fb, (const float*)fv, x0);
+    if (wnan) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    const int64_t w = t * kWTile + jw;
+    if (g == 0 && w < n_rows) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+  };
+  // two tiles per trip, each with its own prefetch registers (no copies at
+  // the back edge)
+  float preA[kWRowRegs], preB[kWRowRegs];
+  load(wave_id < n_tiles ? wave_id : 0, preA);
+  load(wave_id + n_waves < n_tiles ? wave_id + n_waves : 0, preB);
+  for (int64_t t = wave_id; t < n_tiles; t += 2 * n_waves) {
+    tile_body(t, t + 2 * n_waves, preA);
+    if (t + n_waves >= n_tiles) break;
+    tile_body(t + n_waves, t + 3 * n_waves, preB);
+  }
+}
+
 // Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
 // window of each stream is its 5-slot MFCC ring in arrival order
 // (slot (count + d) % 5, oldest first); classify it if count >= 5, then push
@@ -780,6 +956,19 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
     constexpr bool kH3 = (KS0 == 10 && T1 == 4 && T2 == 2 && T3 == 1 && T4 == 1) ||
                          (KS0 == 4 && T1 == 4 && T2 == 4 && T3 == 1 && T4 == 0);
     if constexpr (kH3) {
+      if (mfcc_n == 13 && net.fragh && VAD_FFN_WAVE) {
+        // one resident wave per SIMD pair slot: 2 blocks of 4 waves per CU
+        int64_t wblocks = (n_rows + 4 * kWTile - 1) / (4 * kWTile);
+        const int64_t wcap = 2 * ffn_num_cus();
+        if (wblocks > wcap) wblocks = wcap;
+        if (mode == VAD_FEAT_OFFLINE)
+          hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE>),
+                             dim3((int)wblocks), dim3(256), 0, st, net, in, n_rows, labels);
+        else
+          hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_ANALYSER>),
+                             dim3((int)wblocks), dim3(256), 0, st, net, in, n_rows, labels);
+        return hipGetLastError();
+      }
       if (mfcc_n == 13 && net.fragh) {
         if (mode == VAD_FEAT_OFFLINE)
           hipLaunchKernelGGL((ffn_window_h3_kernel<KS0, T1, T2, T3, T4, NC, 13, VAD_FEAT_OFFLINE>),
