@@ -254,20 +254,17 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 constexpr float kH3Max = 65504.f;  // largest finite f16
 
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
+  // plain conversions, not v_fma_mix* inline asm (one instruction less per
+  // value, but the compiler cannot see an asm VALU write that a following
+  // MFMA reads as an operand, so it could not pad that hazard)
   u4 hw, lw;
 #pragma unroll
   for (int q = 0; q < 8; q += 2) {
     const f2 p = {v[q], v[q + 1]};
     const h2 h = __builtin_convertvector(p, h2);
-    // lo = f16(v - f32(hi)) per half, one mixed-precision fma each (f16
-    // source, f32 addend, one rounding to f16): the same bits as converting
-    // hi back, subtracting in f32 (exact) and converting the difference
-    unsigned l;
-    const unsigned hb = __builtin_bit_cast(unsigned, h);
-    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(l) : "v"(hb), "v"(v[q]));
-    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(l) : "v"(hb), "v"(v[q + 1]));
-    hw[q / 2] = hb;
-    lw[q / 2] = l;
+    const h2 r = __builtin_convertvector(p - __builtin_convertvector(h, f2), h2);
+    hw[q / 2] = __builtin_bit_cast(unsigned, h);
+    lw[q / 2] = __builtin_bit_cast(unsigned, r);
   }
   hi = __builtin_bit_cast(h8, hw);
   lo = __builtin_bit_cast(h8, lw);
