@@ -721,6 +721,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #ifndef VAD_FFN_WAVE
 #define VAD_FFN_WAVE 1  // 0: the 64-window block kernel for the split-f16 topologies
 #endif
+#ifndef VAD_FFN_PF
+#define VAD_FFN_PF 2  // wave kernel: row prefetch depth in tiles (3, 4: no faster)
+#endif
 #ifndef VAD_FFN_WAVE_MFMA_OUT
 #define VAD_FFN_WAVE_MFMA_OUT 0
 #endif
@@ -834,15 +837,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
   };
-  // two tiles per trip, each with its own prefetch registers (no copies at
-  // the back edge)
-  float preA[kWRowRegs], preB[kWRowRegs];
-  load(wave_id < n_tiles ? wave_id : 0, preA);
-  load(wave_id + n_waves < n_tiles ? wave_id + n_waves : 0, preB);
-  for (int64_t t = wave_id; t < n_tiles; t += 2 * n_waves) {
-    tile_body(t, t + 2 * n_waves, preA);
-    if (t + n_waves >= n_tiles) break;
-    tile_body(t + n_waves, t + 3 * n_waves, preB);
+  // VAD_FFN_PF tiles per trip, each with its own prefetch registers (no
+  // copies at the back edge): a tile's rows are loaded PF tiles ahead
+  float pre[VAD_FFN_PF][kWRowRegs];
+#pragma unroll
+  for (int k = 0; k < VAD_FFN_PF; ++k) {
+    const int64_t tk = wave_id + k * n_waves;
+    load(tk < n_tiles ? tk : 0, pre[k]);
+  }
+  for (int64_t t = wave_id; t < n_tiles; t += VAD_FFN_PF * n_waves) {
+#pragma unroll
+    for (int k = 0; k < VAD_FFN_PF; ++k) {
+      const int64_t tk = t + k * n_waves;
+      if (k > 0 && tk >= n_tiles) break;
+      tile_body(tk, tk + VAD_FFN_PF * n_waves, pre[k]);
+    }
   }
 }
 
