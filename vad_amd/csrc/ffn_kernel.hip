@@ -292,7 +292,9 @@ __device__ __forceinline__ float layer_scale(float (&v)[K][8]) {
     for (int q = 0; q < 8; q += 2)
       asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[s][q]), "v"(v[s][q + 1]));
   if (__builtin_amdgcn_ballot_w64(m >= kH3Max) == 0) return 1.f;
-  m = wave_max(m);
+  // wave-uniform from here (readfirstlane): the callers' sc == 1 tests
+  // become scalar branches, not exec-masked regions
+  m = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, wave_max(m))));
   if (!(m < INFINITY)) return 1.f;  // inf stays inf (-> NaN logits, class 0)
   // m >= 65504 is a normal float: 2^(14 - exponent(m)), built from its bits
   const int e = (int)((__builtin_bit_cast(unsigned, m) >> 23) & 0xff) - 127;
@@ -796,8 +798,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     // features (sklearn_analyser.py:52-69 / file_processing.py:51-66): item
     // i = 13 w + c is coefficient c of window w; its rows are R[i + 13 d].
     // A flat coefficient (the analyser's 0/0: mn and d2 NaN) writes its
-    // features as 0 and raises its window's flag -- plain stores of 1, after
-    // the wave's own zeroing stores in LDS order, so no atomics
+    // features as 0 and or-s 1 into its window's flag (a branch-free
+    // ds_or_b32 after the wave's own zeroing stores, in LDS order)
     if (lane < kWTile) FL[lane] = 0;
 #pragma unroll
     for (int r = 0; r < (kWTile * MN + 63) / 64; ++r) {
@@ -807,7 +809,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         const Feat3 ft = feature_triple(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
                                         R[it + 4 * MN], MODE);
         const bool flat = ft.mn != ft.mn;
-        if (flat) FL[w] = 1;
+        __hip_atomic_fetch_or(&FL[w], (int)flat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         float* xw = X + w * XS;
         xw[c] = flat ? 0.f : ft.mn;
         if constexpr (IN > MN) {
