@@ -35,6 +35,10 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFCC_BYTES_PER_FRAME = 160 * 4 + 13 * 4   # new samples in + 13 fp32 out
 FFN_BYTES_PER_FRAME = 13 * 4 + 1          # MFCC row in + uint8 label out
+# SURVEY 8(d) algorithmic flops per frame of the MFCC kernel: FFT 11,520 +
+# power 768 + sparse mel 888 + log 26 + lifter x DCT 676
+MFCC_FLOPS_PER_FRAME = 13878
+VALU_PEAK_TFS = 157.3          # MI355X_MICROARCH.md: peak FP32 (vector)
 
 
 def synth_audio(n_samples, seed, device):
@@ -188,6 +192,13 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": dom_bytes * F,
                          "avg_launch_ms": dom_ms},
+            # the MFCC kernel sits at the fp32 ridge (~20 flop/B): its VALU
+            # ceiling beside the HBM one
+            "compute": {"bound": "valu", "kernel": "mfcc_kernel",
+                        "achieved": MFCC_FLOPS_PER_FRAME * F / (mfcc_ms * 1e-3) / 1e12,
+                        "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": MFCC_FLOPS_PER_FRAME * F / (mfcc_ms * 1e-3) / 1e12 / VALU_PEAK_TFS,
+                        "flops_per_frame": MFCC_FLOPS_PER_FRAME},
             "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms},
         }
         if world == 1 and not args.no_cpu:
