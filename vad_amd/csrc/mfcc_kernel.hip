@@ -111,6 +111,11 @@ constexpr bool kSplitLoads = VAD_SPLIT_LOADS != 0;
 #define VAD_PAIR_FRAMES 1
 #endif
 constexpr bool kPairFrames = VAD_PAIR_FRAMES != 0;
+// paired-frame path: sample chunks requested 1 or 2 tiles ahead
+#ifndef VAD_SAMPLE_DEPTH
+#define VAD_SAMPLE_DEPTH 1
+#endif
+constexpr int kSampleDepth = VAD_SAMPLE_DEPTH;
 
 template <typename TIN, int NZ, bool VEC2, int LEN, int B = 0, int E = NZ>
 __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len_rt, int n2,
@@ -569,6 +574,7 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
     lane_consts(plan, j, L);
     const int64_t flast = n_frames - 1;
     auto pair_base = [&](int64_t t, int& lim) {
+      if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
       const int64_t F = t * kTile + 2 * grp;
       lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
       return src + (F < flast ? F : flast) * frame_stride;
@@ -597,7 +603,8 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
     unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
     (void)stamps;
     int it = 0;
-    for (; tile < t_end; ++tile, ++it) {
+    // one tile; its buffer is refilled with tile + AHEAD's chunks as it frees up
+    auto tile_body = [&](v2f (&buf)[NB], const int AHEAD) {
       unsigned long long st_[kStamps];
       (void)st_;
       const int64_t f0 = tile * kTile;
@@ -612,7 +619,7 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
         prow_b = P + (2 * grp + 1) * kPStride;
       }
       int lim;
-      const TIN* nb = pair_base(tile + 1, lim);
+      const TIN* nb = pair_base(tile + AHEAD, lim);
       v2f u[16], col[32];
       // VAD_PRIO: the younger half leads the first VAD_PRIO segments
 #define VAD_PRIO_AT(k)                                                  \
@@ -685,7 +692,28 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
           }
         }
       }
+        };
+    if constexpr (kSampleDepth == 2) {
+      // two chunk buffers, alternating: a tile's samples are requested two
+      // tiles ahead (+36 VGPRs)
+      v2f buf2[NB];
+      {
+        int lim;
+        const TIN* b1 = pair_base(tile + 1, lim);
+        load_chunks<TIN, 0, NB, LEN>(b1, lim, j, buf2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      while (tile < t_end) {
+        tile_body(buf, 2);
+        ++tile, ++it;
+        if (tile >= t_end) break;
+        tile_body(buf2, 2);
+        ++tile, ++it;
+      }
+    } else {
+      for (; tile < t_end; ++tile, ++it) tile_body(buf, 1);
     }
+
     if constexpr (MODE == kAudioToMfcc) {
       if constexpr (kLateBar2 && DIAG != 10) lds_barrier();  // the last log-mel rows complete
       if (prev_f0 >= 0 && wave < kDctGroups)
@@ -897,6 +925,8 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
         return launch_t<TIN, MODE, 13, true, 400, 1, 5, 5>(plan, src, stride, len, n, out, st);
       if (diag == 9 && stride == 160 && kPairFrames)
         return launch_t<TIN, MODE, 13, true, 400, 1, 9, 5>(plan, src, stride, len, n, out, st);
+      if (diag == 7 && stride == 160 && kPairFrames)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 7, 5>(plan, src, stride, len, n, out, st);
       if (diag == 10 && stride == 160 && kPairFrames)
         return launch_t<TIN, MODE, 13, true, 400, 1, 10, 5>(plan, src, stride, len, n, out, st);
       if (diag == 5 || diag == 8) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
