@@ -35,17 +35,8 @@
 
 namespace vad {
 
-// VAD_WG256: 256-thread workgroups of 32-frame tiles, two per CU (each
-// SIMD hosts one wave of each, so one workgroup's barrier waits and
-// phase 2 overlap the other's FFT); default: one 512-thread workgroup of
-// 64-frame tiles per CU
-#ifndef VAD_WG256
-#define VAD_WG256 0
-#endif
-constexpr int kTile = VAD_WG256 ? 32 : 64;        // frames per workgroup tile
-constexpr int kThreads = VAD_WG256 ? 256 : 512;   // 4 or 8 waves
-constexpr int kWaves = kThreads / 64;
-constexpr int kWgPerCu = VAD_WG256 ? 2 : 1;
+constexpr int kTile = 64;        // frames per workgroup tile
+constexpr int kThreads = 512;    // 8 waves, one workgroup per CU
 constexpr int kGroups = kThreads / 16;  // frames per phase-1 pass
 constexpr int kColStride = 18;   // complex per LDS column: 16-B aligned columns whose
                                  // ds_read_b128 lane groups hit disjoint banks
@@ -111,11 +102,6 @@ constexpr bool kSplitLoads = VAD_SPLIT_LOADS != 0;
 #define VAD_PAIR_FRAMES 1
 #endif
 constexpr bool kPairFrames = VAD_PAIR_FRAMES != 0;
-// paired-frame path: sample chunks requested 1 or 2 tiles ahead
-#ifndef VAD_SAMPLE_DEPTH
-#define VAD_SAMPLE_DEPTH 1
-#endif
-constexpr int kSampleDepth = VAD_SAMPLE_DEPTH;
 
 template <typename TIN, int NZ, bool VEC2, int LEN, int B = 0, int E = NZ>
 __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len_rt, int n2,
@@ -314,24 +300,7 @@ __device__ __forceinline__ float log10_pos(float e) {
 template <int SPEC>
 constexpr int lm_stride() { return SPEC == 1 ? 28 : SPEC == 2 ? 44 : kMaxFilters + 4; }
 constexpr int kLmFloats = kTile * (kMaxFilters + 4);
-// Phase 2b coefficient groups: VAD_DCT8 = 0: waves 0..3 own c = w, w+4, w+8,
-// w+12; VAD_DCT8 = 1: every wave owns c = w, w+8.
-#ifndef VAD_DCT8
-#define VAD_DCT8 0
-#endif
-constexpr int kDctGroups = VAD_DCT8 ? 8 : 4;
-constexpr int kDctPer = 16 / kDctGroups;  // coefficients per group (mfcc_n <= 16)
-// VAD_PRIO = k > 0 (paired-frame loop): waves 4..7 (the arbitration losers,
-// MI355X_MICROARCH.md "Two waves per SIMD") run the first k segments of each
-// tile's FFT at s_setprio 1, the rest at 0, so that both waves of a SIMD
-// finish phase 1 together instead of the younger finishing alone.
-#ifndef VAD_PRIO
-#define VAD_PRIO 0
-#endif
-#ifndef VAD_LATE_BAR2
-#define VAD_LATE_BAR2 0
-#endif
-constexpr bool kLateBar2 = VAD_LATE_BAR2 != 0;
+constexpr int kDctGroups = 4;  // phase 2b: waves 0..3, coefficients c = w, w+4, w+8, w+12
 
 // Phase 2a (runtime plan): frame `lane`, filters [fb, fe) -> log-mel row.
 __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
@@ -361,10 +330,10 @@ __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
 // coefficients c = g + 4 i of group g.
 __device__ __forceinline__ void dct_rt(const MfccDev* __restrict__ plan,
                                        const float* __restrict__ lrow, int g, int mfcc_n,
-                                       float (&acc)[kDctPer]) {
+                                       float (&acc)[4]) {
   const int nf = plan->n_filters;
 #pragma unroll
-  for (int i = 0; i < kDctPer; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int c = g + kDctGroups * i;
     float s0 = 0.f, s1 = 0.f;
     if (c < mfcc_n) {
@@ -391,8 +360,6 @@ __device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
                                               float* __restrict__ lm);
 template <class T, int G>
 __device__ __forceinline__ void dct_code(const float* __restrict__ lm, float (&acc)[4]);
-template <class T, int G>
-__device__ __forceinline__ void dct8_code(const float* __restrict__ lm, float (&acc)[2]);
 
 #include "mel_code.h"
 
@@ -412,26 +379,13 @@ __device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float*
 }
 
 template <class T>
-__device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&acc)[kDctPer]) {
+__device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&acc)[4]) {
   lrow = static_cast<const float*>(__builtin_assume_aligned(lrow, 16));
-  if constexpr (kDctGroups == 8) {
-    switch (g) {
-      case 0: dct8_code<T, 0>(lrow, acc); break;
-      case 1: dct8_code<T, 1>(lrow, acc); break;
-      case 2: dct8_code<T, 2>(lrow, acc); break;
-      case 3: dct8_code<T, 3>(lrow, acc); break;
-      case 4: dct8_code<T, 4>(lrow, acc); break;
-      case 5: dct8_code<T, 5>(lrow, acc); break;
-      case 6: dct8_code<T, 6>(lrow, acc); break;
-      default: dct8_code<T, 7>(lrow, acc); break;
-    }
-  } else {
-    switch (g) {
-      case 0: dct_code<T, 0>(lrow, acc); break;
-      case 1: dct_code<T, 1>(lrow, acc); break;
-      case 2: dct_code<T, 2>(lrow, acc); break;
-      default: dct_code<T, 3>(lrow, acc); break;
-    }
+  switch (g) {
+    case 0: dct_code<T, 0>(lrow, acc); break;
+    case 1: dct_code<T, 1>(lrow, acc); break;
+    case 2: dct_code<T, 2>(lrow, acc); break;
+    default: dct_code<T, 3>(lrow, acc); break;
   }
 }
 
@@ -442,23 +396,9 @@ __device__ __forceinline__ void phase2a(const MfccDev* __restrict__ plan, const 
                                         float* lm, int wave, int lane) {
   const float* prow = P + lane * kPStride;
   float* lrow = lm + lane * lm_stride<SPEC>();
-  if constexpr (kWaves == 8) {
-    if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
-    else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
-    else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
-  } else {  // 4 waves, 32-frame tiles: wave w runs bands 2w and 2w + 1 on lanes 0..31
-    if (lane < kTile) {
-      if constexpr (SPEC == 1) {
-        mel_dispatch<Mel26>(2 * wave, prow, lrow);
-        mel_dispatch<Mel26>(2 * wave + 1, prow, lrow);
-      } else if constexpr (SPEC == 2) {
-        mel_dispatch<Mel40>(2 * wave, prow, lrow);
-        mel_dispatch<Mel40>(2 * wave + 1, prow, lrow);
-      } else {
-        mel_log(plan, prow, plan->wave_fbeg[2 * wave], plan->wave_fend[2 * wave + 1], lrow);
-      }
-    }
-  }
+  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
+  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
+  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
 }
 
 // Phase 2b (waves 0..3): lifter x DCT of the tile's log-mel rows, one frame
@@ -469,9 +409,8 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
                                         int mfcc_n_rt, float* __restrict__ out) {
   constexpr int NC = SPEC == 1 ? Mel26::NC : SPEC == 2 ? Mel40::NC : 0;
   const int mfcc_n = NC > 0 ? NC : mfcc_n_rt;
-  if (kTile < 64 && lane >= kTile) return;
   const float* lrow = lm + lane * lm_stride<SPEC>();
-  float acc[kDctPer];
+  float acc[4];
   if constexpr (SPEC == 1) dct_dispatch<Mel26>(wave, lrow, acc);
   else if constexpr (SPEC == 2) dct_dispatch<Mel40>(wave, lrow, acc);
   else dct_rt(plan, lrow, wave, mfcc_n, acc);
@@ -480,14 +419,11 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
     if (f < n_frames) {
       float* o = out + f * mfcc_n;
 #pragma unroll
-      for (int i = 0; i < kDctPer; ++i)
+      for (int i = 0; i < 4; ++i)
         if (wave + kDctGroups * i < mfcc_n) o[wave + kDctGroups * i] = acc[i];
     }
   } else {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 1; i < kDctPer; ++i) t += acc[i];
-    if (acc[0] == 12345.f) out[0] = t;  // keep the work live
+    if (acc[0] == 12345.f) out[0] = acc[1] + acc[2] + acc[3];  // keep the work live
   }
 }
 
@@ -527,7 +463,7 @@ __device__ __forceinline__ void lds_barrier() {
 // DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
 // HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0>
-__global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
+__global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -603,8 +539,8 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
     unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
     (void)stamps;
     int it = 0;
-    // one tile; its buffer is refilled with tile + AHEAD's chunks as it frees up
-    auto tile_body = [&](v2f (&buf)[NB], const int AHEAD) {
+    // one tile; its buffer is refilled with the next tile's chunks as it frees up
+    auto tile_body = [&](v2f (&buf)[NB]) {
       unsigned long long st_[kStamps];
       (void)st_;
       const int64_t f0 = tile * kTile;
@@ -619,25 +555,10 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
         prow_b = P + (2 * grp + 1) * kPStride;
       }
       int lim;
-      const TIN* nb = pair_base(tile + AHEAD, lim);
+      const TIN* nb = pair_base(tile + 1, lim);
       v2f u[16], col[32];
-      // VAD_PRIO: the younger half leads the first VAD_PRIO segments
-#define VAD_PRIO_AT(k)                                                  \
-  do {                                                                  \
-    if constexpr (VAD_PRIO == (k)) {                                    \
-      __builtin_amdgcn_sched_barrier(0);                                \
-      if (wave >= 4) __builtin_amdgcn_s_setprio((k) == 0 ? 1 : 0);      \
-      __builtin_amdgcn_sched_barrier(0);                                \
-    }                                                                   \
-  } while (0)
-      if constexpr (VAD_PRIO > 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
       VAD_STAMP(0);
       stage_a_at<NZ, LEN, 0>(buf, L, j, u);
-      VAD_PRIO_AT(1);
       VAD_STAMP(1);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
@@ -645,32 +566,22 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
       store_a(u, gscr, j);
       read_b(L, gscr, col);
       __builtin_amdgcn_sched_barrier(0);
-      VAD_PRIO_AT(2);
       VAD_STAMP(2);
       // pass 1's stage A covers the latency of pass 0's transpose reads
       stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
-      VAD_PRIO_AT(3);
-      // VAD_LATE_BAR2: the previous tile's phase 2a must have read P before
-      // this tile's first power row lands; waiting here, not right after
-      // phase 2a, lets a wave run into this tile's stage A meanwhile
-      if constexpr (kLateBar2 && MODE == kAudioToMfcc && DIAG != 10)
-        if (prev_f0 >= 0) lds_barrier();
       VAD_STAMP(3);
       if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
-      VAD_PRIO_AT(4);
       VAD_STAMP(4);
       store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
       read_b(L, gscr, col);
-      VAD_PRIO_AT(5);
       VAD_STAMP(5);
       if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
-      VAD_PRIO_AT(6);
       if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(6);
@@ -681,7 +592,7 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
         VAD_STAMP(8);
         phase2a<SPEC>(plan, P, lm, wave, lane);
         VAD_STAMP(9);
-        if constexpr (!kLateBar2) lds_barrier();  // log-mel rows complete; P and the FFT scratch free
+        lds_barrier();  // log-mel rows complete; P and the FFT scratch free
         VAD_STAMP(10);
         prev_f0 = f0;
         if constexpr (DIAG == 5 || DIAG == 6) {
@@ -693,29 +604,9 @@ __global__ __launch_bounds__(kThreads, kWgPerCu) void mfcc_kernel(
         }
       }
         };
-    if constexpr (kSampleDepth == 2) {
-      // two chunk buffers, alternating: a tile's samples are requested two
-      // tiles ahead (+36 VGPRs)
-      v2f buf2[NB];
-      {
-        int lim;
-        const TIN* b1 = pair_base(tile + 1, lim);
-        load_chunks<TIN, 0, NB, LEN>(b1, lim, j, buf2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      while (tile < t_end) {
-        tile_body(buf, 2);
-        ++tile, ++it;
-        if (tile >= t_end) break;
-        tile_body(buf2, 2);
-        ++tile, ++it;
-      }
-    } else {
-      for (; tile < t_end; ++tile, ++it) tile_body(buf, 1);
-    }
+    for (; tile < t_end; ++tile, ++it) tile_body(buf);
 
     if constexpr (MODE == kAudioToMfcc) {
-      if constexpr (kLateBar2 && DIAG != 10) lds_barrier();  // the last log-mel rows complete
       if (prev_f0 >= 0 && wave < kDctGroups)
         phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
@@ -896,7 +787,7 @@ template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, 
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int cap = num_cus() * kWgPerCu;  // persistent, LDS-bound: kWgPerCu workgroups per CU
+  const int cap = num_cus();  // persistent, LDS-bound: one workgroup per CU
   const int grid = (int)(n_tiles < cap ? n_tiles : cap);
   const size_t smem = mfcc_smem_bytes();
   static bool attr_set = false;

@@ -165,15 +165,13 @@ def emit_code(name, info):
                        f"  // (==0 -> eps), log10")
         out.append("}")
         out.append("")
-    for ng, fname in ((DCT_GROUPS, "dct_code"), (8, "dct8_code")):
-        out += dct_groups(name, d, ng, fname)
+    out += dct_groups(name, d, DCT_GROUPS, "dct_code")
     return "\n".join(out)
 
 
 def dct_groups(name, d, ng, fname):
     """lifter x DCT of a log-mel row for the coefficient groups c = g + ng i
-    (ng = 4: waves 0..3 own four coefficients each; ng = 8: every wave owns
-    one or two)."""
+    (ng = 4: waves 0..3 own four coefficients each)."""
     nf, nc = d.shape[1], d.shape[0]
     per = (nc + ng - 1) // ng
     comp = "xyzw"
