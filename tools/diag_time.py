@@ -28,4 +28,5 @@ for _ in range(5):  # 5 batches of 20 launches: min and median of the batch mean
     ts.append(s.elapsed_time(e) / n * 1e3)
 ts.sort()
 tag = " ".join(f"{k}={v}" for k, v in os.environ.items() if k.startswith("VAD_") and k != "VAD_AMD_LIB")
-print(f"[{tag}] mfcc min {ts[0]:.1f} us  median {ts[2]:.1f} us")
+chk = out.double().abs().sum().item()  # variants must agree exactly
+print(f"[{tag}] mfcc min {ts[0]:.1f} us  median {ts[2]:.1f} us  checksum {chk:.17g}")
