@@ -219,6 +219,12 @@ int vad_simple_features(const float* frames, int64_t n_frames, int32_t frame_len
  * (feed_frame returns None for its first 5 calls, :48-50).
  * ------------------------------------------------------------------------- */
 int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n);
+/* Advance every stream's frame buffer by one hop, in place:
+ *   frames[s, 0 : L-H] <- frames[s, H : L];  frames[s, L-H : L] <- hop[s, 0 : H]
+ * (L = frame_len <= 1024, H = hop_len, 0 < H <= L), i.e. the next frame the
+ * live loop of vad.py:37-49 hands to feed_frame.  One kernel; capturable. */
+int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, const float* hop,
+                        int64_t hop_stride, int32_t hop_len, int64_t n_streams, void* stream);
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);

@@ -412,6 +412,25 @@ def test_stream_batch_matches_clip_path(torch_cuda, golden):
         np.testing.assert_array_equal(got[:, 5:], want[:, :T - 5])
 
 
+@pytest.mark.parametrize("L,H", [(400, 160), (400, 400), (600, 1), (1024, 160)])
+def test_stream_push_hop(torch_cuda, L, H):
+    """vad_stream_push_hop == shift left by H and append the new samples."""
+    import torch
+    from vad_amd import _lib
+    S = 37
+    g = torch.Generator(device="cuda").manual_seed(L + H)
+    frames = torch.randn((S, L + 3), device="cuda", generator=g)  # row stride L + 3
+    hop = torch.randn((S, H + 2), device="cuda", generator=g)
+    want = frames.clone()
+    want[:, :L] = torch.cat([frames[:, H:L], hop[:, :H]], dim=1)
+    _lib.check(_lib.lib().vad_stream_push_hop(_lib.ptr(frames), L + 3, L, _lib.ptr(hop), H + 2, H, S,
+                                              _lib.stream_ptr()), "vad_stream_push_hop")
+    torch.cuda.synchronize()
+    assert torch.equal(frames, want)
+    assert _lib.lib().vad_stream_push_hop(_lib.ptr(frames), L + 3, L, _lib.ptr(hop), H + 2, L + 1, S,
+                                          _lib.stream_ptr()) == _lib.VAD_EINVAL
+
+
 # ---------------------------------------------------------------------------
 # full-size properties (BASELINE config 3 size)
 # ---------------------------------------------------------------------------

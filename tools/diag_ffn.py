@@ -10,7 +10,8 @@ from bench import synth_audio  # noqa: E402
 from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers  # noqa: E402
 from vad_amd.pipeline import VadPipeline  # noqa: E402
 
-topo = TOPOLOGY_REF39 if os.environ.get("VAD_FFN_TOPO") == "ref39" else TOPOLOGY_BL13
+topo = {"ref39": TOPOLOGY_REF39, "bl13c3": (13, 64, 64, 3)}.get(os.environ.get("VAD_FFN_TOPO"),
+                                                                TOPOLOGY_BL13)
 pipe = VadPipeline(FFNClassifier(random_layers(topo, seed=3)))
 F = 1_000_000
 audio = synth_audio(160 * (F - 1) + 401, 1, torch.device("cuda"))

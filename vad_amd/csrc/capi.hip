@@ -487,6 +487,17 @@ int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n) {
   return n_streams * 5 * (int64_t)mfcc_n;
 }
 
+int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, const float* hop,
+                        int64_t hop_stride, int32_t hop_len, int64_t n_streams, void* stream) {
+  if (n_streams < 0 || frame_len <= 0 || frame_len > 1024 || hop_len <= 0 || hop_len > frame_len ||
+      frame_stride < frame_len || hop_stride < hop_len)
+    return VAD_EINVAL;
+  if (n_streams == 0) return VAD_OK;
+  if (!frames || !hop) return VAD_EINVAL;
+  return (int)launch_stream_push(frames, frame_stride, frame_len, hop, hop_stride, hop_len, n_streams,
+                                 (hipStream_t)stream);
+}
+
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream) {

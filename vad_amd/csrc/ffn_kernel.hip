@@ -321,9 +321,8 @@ __device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1
 
 // out[mt] = bias + sum_s lo*hi + hi*lo + hi*hi (small terms first) on inputs
 // v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
-template <int TO, int KS, class FB>
-__device__ __forceinline__ void dense_h3(const u4 (&A)[TO * KS][2], FB b, float (&v)[KS][8],
-                                         f32x4 (&out)[TO], bool relu) {
+template <int TO, int KS, class FB, class FH>
+__device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu) {
   const float sc = layer_scale<KS>(v);
   h8 bh[KS], bl[KS];
 #pragma unroll
@@ -333,19 +332,19 @@ __device__ __forceinline__ void dense_h3(const u4 (&A)[TO * KS][2], FB b, float 
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int mt = 0; mt < TO; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][1]), bh[s],
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A.get(mt * KS + s, 1)), bh[s],
                                                          s == 0 ? init[mt] : acc[mt], 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int mt = 0; mt < TO; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bl[s],
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A.get(mt * KS + s, 0)), bl[s],
                                                          acc[mt], 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
       for (int mt = 0; mt < TO; ++mt)
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A[mt * KS + s][0]), bh[s],
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A.get(mt * KS + s, 0)), bh[s],
                                                          acc[mt], 0, 0, 0);
   };
   f32x4 bias[TO], acc[TO];
@@ -400,35 +399,44 @@ __device__ __forceinline__ void load_fragh(const uint32_t* __restrict__ fragh, i
   }
 }
 
-template <int N, int OFF, int M>
-__device__ __forceinline__ const u4 (&frag_slice(const u4 (&fh)[M][2]))[N][2] {
-  return *reinterpret_cast<const u4(*)[N][2]>(&fh[OFF]);
-}
+// Split-f16 weight fragments: slot sl, half h (0 = hi, 1 = lo) of this
+// lane, from registers (FragRegs) or from a workgroup-shared LDS copy
+// (FragLds, the plan's [slot][half][lane] layout).
+struct FragRegs {
+  const u4 (*p)[2];
+  __device__ u4 get(int sl, int h) const { return p[sl][h]; }
+  __device__ FragRegs at(int off) const { return {p + off}; }
+};
+struct FragLds {
+  const u4* p;
+  int lane;
+  __device__ u4 get(int sl, int h) const { return p[(2 * sl + h) * 64 + lane]; }
+  __device__ FragLds at(int off) const { return {p + 2 * off * 64, lane}; }
+};
 
 // Forward of one 16-window tile: x0 holds the layer-0 inputs of K-step s,
 // k = 8g + q (g = lane >> 4).
-template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV, bool NOVL = false>
-__device__ __forceinline__ f32x4 mlp_forward_h3(
-    const u4 (&fh)[HTopo<Topo<KS0, T1, T2, T3, T4, NC, NOVL>, KS0, T1, T2, T3, T4>::NS][2], FB fb, FV fv,
-    float (&x0)[(4 * KS0 + 31) / 32][8]) {
+template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV, bool NOVL = false,
+          class FH>
+__device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)[(4 * KS0 + 31) / 32][8]) {
   using TP = Topo<KS0, T1, T2, T3, T4, NC, NOVL>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
   f32x4 h1[T1];
-  dense_h3<T1, HP::K0, FB>(frag_slice<HP::S0, 0>(fh), fb, x0, h1, TP::NL > 1);
+  dense_h3<T1, HP::K0, FB>(fh, fb, x0, h1, TP::NL > 1);
   if constexpr (TP::NL == 1) return h1[0];
   else if constexpr (TP::NL == 2 && TP::VL) return valu_out_layer<TP, T1, FV>(fv, h1);
   else {
     float v1[HP::K1][8];
     acts_of<T1>(h1, v1);
     f32x4 h2[T2];
-    dense_h3<T2, HP::K1, FB>(frag_slice<HP::S1, HP::S0>(fh), fb + 4 * T1, v1, h2, TP::NL > 2);
+    dense_h3<T2, HP::K1, FB>(fh.at(HP::S0), fb + 4 * T1, v1, h2, TP::NL > 2);
     if constexpr (TP::NL == 2) return h2[0];
     else if constexpr (TP::NL == 3 && TP::VL) return valu_out_layer<TP, T2, FV>(fv, h2);
     else {
       float v2[HP::K2][8];
       acts_of<T2>(h2, v2);
       f32x4 h3[T3];
-      dense_h3<T3, HP::K2, FB>(frag_slice<HP::S2, HP::S0 + HP::S1>(fh), fb + 4 * (T1 + T2), v2, h3,
+      dense_h3<T3, HP::K2, FB>(fh.at(HP::S0 + HP::S1), fb + 4 * (T1 + T2), v2, h3,
                                TP::NL > 3);
       if constexpr (TP::NL == 3) return h3[0];
       else if constexpr (TP::VL) return valu_out_layer<TP, T3, FV>(fv, h3);
@@ -436,7 +444,7 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(
         float v3[HP::K3][8];
         acts_of<T3>(h3, v3);
         f32x4 h4[T4];
-        dense_h3<T4, HP::K3, FB>(frag_slice<HP::S3, HP::S0 + HP::S1 + HP::S2>(fh), fb + 4 * (T1 + T2 + T3),
+        dense_h3<T4, HP::K3, FB>(fh.at(HP::S0 + HP::S1 + HP::S2), fb + 4 * (T1 + T2 + T3),
                                  v3, h4, false);
         return h4[0];
       }
@@ -674,7 +682,7 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
         }
       }
       if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
-      else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(fh, (const float*)fb, (const float*)fv, x0);
+      else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(FragRegs{fh}, (const float*)fb, (const float*)fv, x0);
       if (wnan[buf][wl]) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
     } else {
       float x[KS0];
@@ -729,12 +737,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #ifndef VAD_FFN_WAVE_MFMA_OUT
 #define VAD_FFN_WAVE_MFMA_OUT 0
 #endif
+// Residency of the wave kernel per topology (measured per 1M windows):
+// 39-64-32-16-3 keeps its split-f16 weight fragments in a workgroup-shared
+// LDS copy and runs 3 waves per SIMD at 168 VGPRs (75 vs 81 us with the
+// fragments in VGPRs at 2 waves); 13-64-64-2 is as fast either way (67 us)
+// and keeps them in VGPRs at 2 waves (LDS at 2 waves: 72.5 us; at 4 waves
+// the 128-VGPR budget spills: 140 us).  With more than two classes its
+// output layer no longer fits beside the VGPR fragments (scratch spills:
+// 101 us for 13-64-64-3), so those read the fragments from LDS too (78 us).
+template <int KS0, int NC>
+struct WaveResidency {
+  static constexpr bool kLdsFrags = KS0 == 10 || NC > 2;
+  static constexpr int kWavesPerSimd = KS0 == 10 ? 3 : 2;
+};
 constexpr int kWTile = 16;                       // windows per wave tile
 constexpr int kWRows = (kWTile + 4) * 13;        // staged MFCC floats per tile (260)
 constexpr int kWRowRegs = (kWRows + 63) / 64;    // 5 per lane
 
 template <int KS0, int T1, int T2, int T3, int T4, int NC, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void ffn_wave_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResidency<KS0, NC>::kWavesPerSimd))) void ffn_wave_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
   // VAD_FFN_WAVE_MFMA_OUT: the output layer on the MFMA too (the plan's
   // fragh holds its slots after the hidden layers'); default: bl13's on the
@@ -759,9 +780,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
   float fa[1];
   float fb[TP::NB];
   float fv[TP::NV + TP::NVB + 1];
-  u4 fh[HP::NS][2];
   load_frags<TP, true>(net.frag, lane, fa, fb, fv);
-  load_fragh<HP>(net.fragh, lane, fh);
+  constexpr bool kLdsFrags = WaveResidency<KS0, NC>::kLdsFrags;
+  __shared__ u4 fh_s[kLdsFrags ? HP::NS * 2 * 64 : 1];
+  u4 fh_r[kLdsFrags ? 1 : HP::NS][2];
+  if constexpr (kLdsFrags) {
+    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 256) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
+    __syncthreads();
+  } else {
+    load_fragh<HP>(net.fragh, lane, *reinterpret_cast<u4(*)[HP::NS][2]>(fh_r));
+  }
+  const auto fh = [&] {
+    if constexpr (kLdsFrags) return FragLds{fh_s, lane};
+    else return FragRegs{fh_r};
+  }();
   // feature columns IN .. 32 K0 - 1 are read by layer 0 and stay 0
   for (int i = lane; i < kWTile * XS; i += 64) X[i] = 0.f;
 
@@ -968,7 +1000,7 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
       if (mfcc_n == 13 && net.fragh && VAD_FFN_WAVE) {
         // one resident wave per SIMD pair slot: 2 blocks of 4 waves per CU
         int64_t wblocks = (n_rows + 4 * kWTile - 1) / (4 * kWTile);
-        const int64_t wcap = 2 * ffn_num_cus();
+        const int64_t wcap = WaveResidency<KS0, NC>::kWavesPerSimd * ffn_num_cus();
         if (wblocks > wcap) wblocks = wcap;
         if (mode == VAD_FEAT_OFFLINE)
           hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE>),

@@ -71,6 +71,8 @@ hipError_t launch_ffn(const FfnDev& net, int src, const float* in, int64_t n_row
                       int mode, uint8_t* labels, hipStream_t st);
 hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring, int* count,
                              int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st);
+hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const float* hop, int64_t hstride,
+                              int hlen, int64_t n_streams, hipStream_t st);
 hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
                            hipStream_t st);
 hipError_t launch_simple_features(const float* frames, int64_t n_frames, int frame_len,

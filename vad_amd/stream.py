@@ -3,8 +3,9 @@
 Each of S streams behaves like its own ``SKLearnAnalyzer.feed_frame`` loop
 (realtime_analysis/sklearn_analyser.py:46-82) fed with the 400-sample frame
 that ends at the newest sample, advanced one hop (160 samples = 10 ms) per
-step.  One step = frame assembly (carry + new hop) + the HIP MFCC kernel +
-the window-feature/FFN MFMA kernel, all on device, replayable as one hipGraph.
+step.  One step = three HIP kernels -- frame assembly (shift by one hop,
+append the new samples, in place), MFCC, window features + FFN -- replayable
+as one hipGraph.
 
 labels[s] after a step is the class of stream s's window centred three steps
 earlier, or 255 during each stream's first five steps (feed_frame returns
@@ -37,7 +38,6 @@ class StreamBatch:
         self.count = torch.zeros((S,), dtype=torch.int32, device=dev)
         self.labels = torch.full((S,), 255, dtype=torch.uint8, device=dev)
         self.scratch = torch.zeros((S, C), dtype=torch.float32, device=dev)
-        self._tmp = torch.zeros((S, L - H), dtype=torch.float32, device=dev)
         self.graph = None
 
     def prime(self, carry):
@@ -53,10 +53,10 @@ class StreamBatch:
 
     def _body(self):
         L, H = self.cfg.frame_size, self.cfg.hop
-        self._tmp.copy_(self.frames[:, H:])
-        self.frames[:, :L - H].copy_(self._tmp)
-        self.frames[:, L - H:].copy_(self.hop_in)
-        _lib.check(_lib.lib().vad_stream_step(
+        lib = _lib.lib()
+        _lib.check(lib.vad_stream_push_hop(_lib.ptr(self.frames), L, L, _lib.ptr(self.hop_in), H, H,
+                                           self.n, _lib.stream_ptr()), "vad_stream_push_hop")
+        _lib.check(lib.vad_stream_step(
             self.plan.handle, self.ffn.plan.handle, _lib.ptr(self.frames), L, L, self.n,
             _lib.ptr(self.ring), _lib.ptr(self.count), _lib.ptr(self.labels),
             _lib.ptr(self.scratch), _lib.stream_ptr()), "vad_stream_step")
