@@ -147,16 +147,22 @@ def main():
     # around `steps` back-to-back launches of one kernel (an event record
     # between two kernels idles the GPU for ~5 us, so the timed steps carry
     # none)
-    def kernel_ms(fn):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(args.steps):
-            fn()
-        b.record(stream)
+    # (batches of 10 launches between event pairs: the mean over all of them,
+    # and p10 / p50 / p90 of the batch means)
+    def kernel_ms(fn, batch=10):
+        nb = max(1, args.steps // batch)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(nb + 1)]
+        ev[0].record(stream)
+        for i in range(nb):
+            for _ in range(batch):
+                fn()
+            ev[i + 1].record(stream)
         torch.cuda.synchronize()
-        return a.elapsed_time(b) / args.steps
-    mfcc_ms = kernel_ms(lambda: pipe.mfcc(audio, out=mfcc))
-    ffn_ms = kernel_ms(lambda: ffn_plan.window_labels(mfcc, out=labels))
+        per = sorted(ev[i].elapsed_time(ev[i + 1]) / batch for i in range(nb))
+        pct = {f"p{q}": per[min(nb - 1, int(q / 100 * nb))] for q in (10, 50, 90)}
+        return ev[0].elapsed_time(ev[nb]) / (nb * batch), pct
+    mfcc_ms, mfcc_pct = kernel_ms(lambda: pipe.mfcc(audio, out=mfcc))
+    ffn_ms, ffn_pct = kernel_ms(lambda: ffn_plan.window_labels(mfcc, out=labels))
 
     if rank == 0:
         value = world * F * args.steps / el
@@ -200,6 +206,7 @@ def main():
                         "frac": MFCC_FLOPS_PER_FRAME * F / (mfcc_ms * 1e-3) / 1e12 / VALU_PEAK_TFS,
                         "flops_per_frame": MFCC_FLOPS_PER_FRAME},
             "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms},
+            "kernels_ms_pct": {"mfcc_kernel": mfcc_pct, "ffn_kernel": ffn_pct},
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(layers)

@@ -231,7 +231,8 @@ def test_ffn_split_f16_rescale(torch_cuda, golden):
 
 
 def test_window_labels_random_nets_long_clip(torch_cuda):
-    """Window labels of both specialised topologies (split-f16 MFMA path) on a
+    """Window labels of both specialised topologies (split-f16 MFMA path; a
+    3-class 13-64-64-3 runs the bl13 shape with its fragments in LDS) on a
     20k-frame synthetic clip with digital silence (NaN windows) vs the
     oracle's forward on the same device features, where the oracle's top-2
     margin exceeds 1e-3."""
@@ -240,7 +241,7 @@ def test_window_labels_random_nets_long_clip(torch_cuda):
     from vad_amd.pipeline import VadPipeline
     F = 20000
     clip = O.synth_clip(160 * (F - 1) + 401, seed=7).astype(np.float32)
-    for topo in (TOPOLOGY_BL13, TOPOLOGY_REF39):
+    for topo in (TOPOLOGY_BL13, TOPOLOGY_REF39, (13, 64, 64, 3)):
         lay = random_layers(topo, seed=3)
         pipe = VadPipeline(FFNClassifier(lay))
         m = pipe.mfcc(torch_cuda.from_numpy(clip).cuda())
