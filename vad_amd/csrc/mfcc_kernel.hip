@@ -443,6 +443,31 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
   } while (0)
 constexpr int kStamps = 11;
 
+
+// Milestone priorities (paired-frame loop, fp32 input): a wave lowers its
+// issue priority (s_setprio 3 -> 0) each time it passes a phase-1 milestone
+// (tile start, pass-0 transpose issued, pass-1 stage A, pass-0 power row),
+// so the younger wave of a SIMD, which loses every tie on age, gets the VALU
+// until it reaches the same milestone and the two reach the first barrier
+// closer together: -7 us per 1M frames on fp32 input, +3.5 us on int16
+// (left off there).
+template <typename TIN>
+constexpr bool kMilestonePrio = std::is_same_v<TIN, float>;
+
+// (Placements measured: 3/2/1/0 at these four; 3/2/-/1 + 0 after the pass-1
+// power row +4 us; 3/-/2/1 + 0 there the same.  Spreading the DCT over all
+// 8 waves, or running it at the top of the next tile, is slower with them,
+// and so is giving the younger waves priority 1 in phase 2a or in the last
+// phase-1 segment.)
+#define VAD_MILESTONE(k)                                 \
+  do {                                                   \
+    if constexpr (kMilestonePrio<TIN>) {                 \
+      __builtin_amdgcn_sched_barrier(0);                 \
+      __builtin_amdgcn_s_setprio(k);                     \
+      __builtin_amdgcn_sched_barrier(0);                 \
+    }                                                    \
+  } while (0)
+
 constexpr size_t kPBytes = (size_t)kTile * kPStride * sizeof(float);          // 66,560
 constexpr size_t kScrBytes = (size_t)kGroups * kGroupScratch * sizeof(v2f);  // 73,728
 constexpr size_t kLmBytes = (size_t)kLmFloats * sizeof(float);               // 17,408
@@ -558,6 +583,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       const TIN* nb = pair_base(tile + 1, lim);
       v2f u[16], col[32];
       VAD_STAMP(0);
+      VAD_MILESTONE(3);
       stage_a_at<NZ, LEN, 0>(buf, L, j, u);
       VAD_STAMP(1);
       __builtin_amdgcn_sched_barrier(0);
@@ -567,17 +593,20 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       read_b(L, gscr, col);
       __builtin_amdgcn_sched_barrier(0);
       VAD_STAMP(2);
+      VAD_MILESTONE(2);
       // pass 1's stage A covers the latency of pass 0's transpose reads
       stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
       VAD_STAMP(3);
+      VAD_MILESTONE(1);
       if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
       __builtin_amdgcn_sched_barrier(0);
       load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
       VAD_STAMP(4);
+      VAD_MILESTONE(0);
       store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
       read_b(L, gscr, col);
       VAD_STAMP(5);
