@@ -332,6 +332,7 @@ int vad_ffn_plan_destroy(vad_ffn_plan* p) {
 
 struct vad_tree_plan {
   TreeNode* nodes_dev;
+  TreeNodeC* cnodes_dev;  // compact copy for the LDS-resident window walk
   int n_nodes;
   int n_features;
 };
@@ -360,12 +361,32 @@ int vad_tree_plan_create(int32_t n_nodes, const int32_t* feature, const double* 
       return VAD_EINVAL;
     }
   }
+  std::vector<TreeNodeC> c((size_t)n_nodes);
+  for (int i = 0; i < n_nodes; ++i) {
+    const TreeNode& nd = h[i];
+    TreeNodeC& cn = c[i];
+    float f = (float)nd.threshold;  // round down to a float: x <= f  <=>  (double)x <= threshold
+    if ((double)f > nd.threshold) f = nextafterf(f, -INFINITY);
+    cn.thr = f;
+    cn.feature = nd.feature >= 0 ? (nd.feature | (nd.nan_left ? 1 << 30 : 0)) : -1 - nd.leaf;
+    cn.left = nd.left;
+    cn.right = nd.right;
+  }
   vad_tree_plan* p = (vad_tree_plan*)calloc(1, sizeof(vad_tree_plan));
   if (!p) return VAD_ENOMEM;
   hipError_t e = hipMalloc((void**)&p->nodes_dev, h.size() * sizeof(TreeNode));
   if (e != hipSuccess) { free(p); return (int)e; }
-  e = hipMemcpy(p->nodes_dev, h.data(), h.size() * sizeof(TreeNode), hipMemcpyHostToDevice);
+  e = hipMalloc((void**)&p->cnodes_dev, c.size() * sizeof(TreeNodeC));
   if (e != hipSuccess) { (void)hipFree(p->nodes_dev); free(p); return (int)e; }
+  e = hipMemcpy(p->nodes_dev, h.data(), h.size() * sizeof(TreeNode), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(p->cnodes_dev, c.data(), c.size() * sizeof(TreeNodeC), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(p->nodes_dev);
+    (void)hipFree(p->cnodes_dev);
+    free(p);
+    return (int)e;
+  }
   p->n_nodes = n_nodes;
   p->n_features = n_features;
   *out = p;
@@ -375,6 +396,7 @@ int vad_tree_plan_create(int32_t n_nodes, const int32_t* feature, const double* 
 int vad_tree_plan_destroy(vad_tree_plan* p) {
   if (!p) return VAD_OK;
   (void)hipFree(p->nodes_dev);
+  (void)hipFree(p->cnodes_dev);
   free(p);
   return VAD_OK;
 }
@@ -396,7 +418,7 @@ int vad_features_tree(const vad_tree_plan* t, const float* mfcc, int64_t n_frame
   const int64_t rows = n_frames > 5 ? n_frames - 5 : 0;
   if (rows == 0) return VAD_OK;
   if (!mfcc || !labels) return VAD_EINVAL;
-  return (int)launch_tree_windows(t->nodes_dev, t->n_nodes, mfcc, rows, mfcc_n, mode, labels,
+  return (int)launch_tree_windows(t->nodes_dev, t->cnodes_dev, t->n_nodes, mfcc, rows, mfcc_n, mode, labels,
                                   (hipStream_t)stream);
 }
 

@@ -61,6 +61,17 @@ struct TreeNode {
   double threshold;
 };
 
+// Compact node for the LDS-resident walk: 16 B.  feature >= 0: internal,
+// bit 30 = missing_go_to_left, bits 0..15 = feature; feature < 0: leaf of
+// class -1 - feature.  thr = the largest float <= threshold, so for a float
+// x, x <= thr exactly when (double)x <= threshold (sklearn's comparison).
+struct TreeNodeC {
+  float thr;
+  int feature;
+  int left;
+  int right;
+};
+
 // Launchers (defined in the .hip translation units).
 size_t mfcc_smem_bytes();
 hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
@@ -84,7 +95,8 @@ int64_t format_csv_rows(const float* rows, int64_t n_rows, int n_cols, double la
                         int64_t buf_size);
 hipError_t launch_tree_rows(const TreeNode* nodes, int n_nodes, const float* x, int64_t n, int dim,
                             uint8_t* labels, hipStream_t st);
-hipError_t launch_tree_windows(const TreeNode* nodes, int n_nodes, const float* mfcc, int64_t n_rows,
+hipError_t launch_tree_windows(const TreeNode* nodes, const TreeNodeC* cnodes, int n_nodes,
+                               const float* mfcc, int64_t n_rows,
                                int mfcc_n, int mode, uint8_t* labels, hipStream_t st);
 
 // NaN-keeping ReLU (numpy / Keras keep NaN; fmaxf would drop it).
