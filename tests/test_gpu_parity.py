@@ -528,6 +528,37 @@ def test_tree_window_labels_on_clip(torch_cuda, golden):
     assert np.array_equal(g["classes"][lab], O.tree_predict(tree, window_features(m).cpu().numpy()))
 
 
+def test_tree_window_threshold_ties(torch_cuda, golden):
+    """The LDS walk compares float features with thresholds rounded down to
+    float; sklearn compares in double.  Thresholds set exactly to feature
+    values the windows produce, and one double ulp above / below them, must
+    give the oracle's (double-comparison) labels."""
+    from vad_amd.plan import window_features
+    from vad_amd.tree import TreeClassifier
+    g, _ = _tree(golden)
+    clip = O.synth_clip(O.samples_for_frames(2000), 43)
+    from vad_amd.pipeline import VadPipeline
+    m = VadPipeline().mfcc(torch_cuda.from_numpy(clip).cuda())
+    feats = window_features(m).cpu().numpy()
+    rng = np.random.default_rng(5)
+    thr = g["threshold"].copy()
+    inner = np.nonzero(g["feature"] >= 0)[0]
+    for k, i in enumerate(inner):  # each internal node: a feature value seen at that node's feature
+        col = feats[:, g["feature"][i]]
+        v = float(col[rng.integers(len(col))])
+        if not np.isfinite(v):
+            continue
+        thr[i] = (v, np.nextafter(v, np.inf), np.nextafter(v, -np.inf))[k % 3]
+    tree = {"feature": g["feature"], "threshold": thr, "left": g["left"], "right": g["right"],
+            "leaf": g["leaf"], "nan_left": g["nan_left"], "classes": g["classes"],
+            "n_features": int(g["n_features"])}
+    t = TreeClassifier(g["feature"], thr, g["left"], g["right"], g["leaf"], g["nan_left"],
+                       g["classes"], int(g["n_features"]))
+    got = g["classes"][t.window_labels(m).cpu().numpy()]
+    assert np.array_equal(got, O.tree_predict(tree, feats))
+    assert np.array_equal(t.predict(feats), O.tree_predict(tree, feats))  # the global row walk
+
+
 class _HostTree:
     """The same sklearn tree kept on the host (the reference's call path)."""
 
