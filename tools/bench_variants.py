@@ -4,6 +4,7 @@
   C3m  MFCC only, 1M frames, fp32 vs int16 PCM input      frames/s, kernel us
   C3f  MFCC + FFN, 1M frames, ref39 vs bl13               frames/s
   C5   512 analyser streams, one hop per step, hipGraph   us per hop (all streams)
+  tree / SimpleAnalyser feature kernels                   kernel us
 
 Kernel times are HIP events on the launching stream around N repeats after
 warm-up; inputs are device-resident.  Prints one JSON object.
@@ -92,6 +93,23 @@ def main():
     tt = timed(lambda: tree.window_labels(out, out=lab), max(10, a.reps // 2))
     res["C3_mfcc_tree"] = {"frames_per_s": F / t, "us": t * 1e6, "tree_kernel_us": tt * 1e6,
                            "nodes": int(len(tree.feature))}
+
+    # SimpleAnalyser per-frame features (fp64: stEnergy, stZCR, std|fft|, 4 bands),
+    # 100k frames of 400 samples (fft 512), one launch
+    from vad_amd import _lib
+    from vad_amd.simple_analyser import SimpleAnalyser
+    sa = SimpleAnalyser(16000, 400, 10)
+    Fs = 100_000
+    fr = x[: 160 * (Fs - 1) + 400].unfold(0, 400, 160).contiguous()
+    sf = torch.empty((Fs, 7), dtype=torch.float64, device=dev)
+    lib = _lib.lib()
+
+    def simple():
+        _lib.check(lib.vad_simple_features(_lib.ptr(fr), Fs, 400, 400, sa._fft_len(),
+                                           sa.fft_extended_zeros, sa.fftn_for_band, 4, _lib.ptr(sf),
+                                           _lib.stream_ptr()), "vad_simple_features")
+    t = timed(simple, a.reps)
+    res["simple_features_100k"] = {"frames_per_s": Fs / t, "us": t * 1e6}
 
     # C5: 512 streams, one 10 ms hop per step, replayed hipGraph
     S = 512

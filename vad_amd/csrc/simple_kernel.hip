@@ -12,9 +12,9 @@
 // (:386-400), stEnergy / stZCR restated from pyAudioAnalysis
 // (audioFeatureExtraction.stEnergy / stZCR; the package is absent here).
 //
-// One 256-thread workgroup per frame: samples and the complex spectrum in
-// LDS; a radix-2 FFT when L is a power of two (the reference's 400-sample
-// frames: L = 512), a direct DFT otherwise (e.g. 401 samples: L = 513).
+// Power-of-two L (the reference's 400-sample frames: L = 512): one wave per
+// frame (simple_features_wave_kernel, below); otherwise (e.g. 401 samples:
+// L = 513) one 256-thread workgroup per frame with a direct DFT.
 #include "vad_common.h"
 
 namespace vad {
@@ -22,15 +22,15 @@ namespace vad {
 constexpr int kSimpleThreads = 256;
 constexpr int kSimpleMaxL = 1024;
 
+// Workgroup sum: a butterfly within each wave (DPP / permute shuffles),
+// then the four wave partials in a fixed order (deterministic).
 __device__ double block_sum(double v, double* red) {
-  const int t = threadIdx.x;
-  red[t] = v;
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
   __syncthreads();
-  for (int s = kSimpleThreads / 2; s > 0; s >>= 1) {
-    if (t < s) red[t] += red[t + s];
-    __syncthreads();
-  }
-  const double r = red[0];
+  const double r = (red[0] + red[1]) + (red[2] + red[3]);
   __syncthreads();
   return r;
 }
@@ -39,11 +39,16 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     const float* __restrict__ frames, int64_t n_frames, int frame_len, int64_t frame_stride,
     int L, int pad, int band_bins, int n_bands, double* __restrict__ out) {
   __shared__ double re[kSimpleMaxL], im[kSimpleMaxL];
-  __shared__ double red[kSimpleThreads];
+  __shared__ double twc[kSimpleMaxL / 2], tws[kSimpleMaxL / 2];  // exp(-2 pi i j / L), j < L/2
+  __shared__ double red[kSimpleThreads / 64];
   const int t = threadIdx.x;
   const bool pow2 = (L & (L - 1)) == 0;
   int log2L = 0;
   while ((1 << log2L) < L) ++log2L;
+  if (pow2) {  // stage len's twiddle k / len is table entry k L / len (exact: powers of two)
+    for (int j = t; j < (L >> 1); j += kSimpleThreads) sincospi(-2.0 * (double)j / (double)L, &tws[j], &twc[j]);
+    __syncthreads();
+  }
   const int n_out = 3 + n_bands;
   for (int64_t f = blockIdx.x; f < n_frames; f += gridDim.x) {
     const float* x = frames + f * frame_stride;
@@ -81,8 +86,8 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
         for (int b = t; b < (L >> 1); b += kSimpleThreads) {
           const int grp = b / half, k = b - grp * half;
           const int i0 = grp * len + k, i1 = i0 + half;
-          double s, c;
-          sincospi(-2.0 * (double)k / (double)len, &s, &c);
+          const int tw = k * (L / len);
+          const double c = twc[tw], s = tws[tw];
           const double xr = re[i1] * c - im[i1] * s, xi = re[i1] * s + im[i1] * c;
           const double ar = re[i0], ai = im[i0];
           re[i0] = ar + xr;
@@ -145,10 +150,125 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
   }
 }
 
+// Power-of-two L (the reference's 400-sample frames: L = 512): one wave per
+// frame, no workgroup barriers -- the wave's own LDS slice holds its
+// spectrum (LDS operations are in order within a wave), reductions are wave
+// butterflies, and the twiddle table is shared by the workgroup.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(kSimpleThreads) void simple_features_wave_kernel(
+    const float* __restrict__ frames, int64_t n_frames, int frame_len, int64_t frame_stride,
+    int L, int pad, int band_bins, int n_bands, double* __restrict__ out) {
+  extern __shared__ double sm[];  // [L/2] cos, [L/2] sin, then per wave [L] re, [L] im
+  double* twc = sm;
+  double* tws = sm + (L >> 1);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  double* re = sm + L + wave * 2 * L;
+  double* im = re + L;
+  int log2L = 0;
+  while ((1 << log2L) < L) ++log2L;
+  for (int j = threadIdx.x; j < (L >> 1); j += kSimpleThreads)
+    sincospi(-2.0 * (double)j / (double)L, &tws[j], &twc[j]);
+  __syncthreads();
+  const int n_out = 3 + n_bands;
+  const int64_t nw = (int64_t)gridDim.x * (kSimpleThreads / 64);
+  for (int64_t f = (int64_t)blockIdx.x * (kSimpleThreads / 64) + wave; f < n_frames; f += nw) {
+    const float* x = frames + f * frame_stride;
+    double e = 0.0, z = 0.0;
+    for (int i = lane; i < frame_len; i += 64) {
+      const double v = (double)x[i];
+      e += v * v;
+      if (i + 1 < frame_len) {
+        const double w = (double)x[i + 1];
+        const double sv = (double)((v > 0.0) - (v < 0.0)), sw = (double)((w > 0.0) - (w < 0.0));
+        z += fabs(sw - sv);
+      }
+    }
+    e = wave_sum(e);
+    z = wave_sum(z);
+    for (int i = lane; i < L; i += 64) {
+      const int sidx = i - pad;
+      const double v = (sidx >= 0 && sidx < frame_len) ? (double)x[sidx] : 0.0;
+      const int r = (int)(__builtin_bitreverse32((unsigned)i) >> (32 - log2L));
+      re[r] = v;
+      im[r] = 0.0;
+    }
+    wave_lds_sync();
+    for (int len = 2; len <= L; len <<= 1) {  // iterative radix-2 DIT, as the block kernel
+      const int half = len >> 1;
+      for (int b = lane; b < (L >> 1); b += 64) {
+        const int grp = b / half, k = b - grp * half;
+        const int i0 = grp * len + k, i1 = i0 + half;
+        const int tw = k * (L / len);
+        const double c = twc[tw], s = tws[tw];
+        const double xr = re[i1] * c - im[i1] * s, xi = re[i1] * s + im[i1] * c;
+        const double ar = re[i0], ai = im[i0];
+        re[i0] = ar + xr;
+        im[i0] = ai + xi;
+        re[i1] = ar - xr;
+        im[i1] = ai - xi;
+      }
+      wave_lds_sync();
+    }
+    double mag_sum = 0.0;
+    for (int k = lane; k < L; k += 64) {
+      const double m = sqrt(re[k] * re[k] + im[k] * im[k]);
+      mag_sum += m;
+      re[k] = m;
+    }
+    const double mean = wave_sum(mag_sum) / (double)L;
+    double ssd = 0.0;
+    for (int k = lane; k < L; k += 64) {
+      const double d = re[k] - mean;
+      ssd += d * d;
+    }
+    ssd = wave_sum(ssd);
+    double* o = out + f * n_out;
+    for (int b = 0; b < n_bands; ++b) {
+      double be = 0.0;
+      for (int k = b * band_bins + lane; k < (b + 1) * band_bins; k += 64) be += re[k] * re[k];
+      be = wave_sum(be);
+      if (lane == 0) o[3 + b] = be / (double)band_bins;
+    }
+    if (lane == 0) {
+      o[0] = e / (double)frame_len;
+      o[1] = (z * 0.5) / ((double)frame_len - 1.0) * (double)frame_len;
+      o[2] = sqrt(ssd / (double)L);
+    }
+    wave_lds_sync();  // the next frame overwrites re / im
+  }
+}
+
 hipError_t launch_simple_features(const float* frames, int64_t n_frames, int frame_len,
                                   int64_t frame_stride, int L, int pad, int band_bins, int n_bands,
                                   double* out, hipStream_t st) {
   if (n_frames <= 0) return hipSuccess;
+  if ((L & (L - 1)) == 0) {
+    int64_t blocks = (n_frames + 3) / 4;
+    if (blocks > 2048) blocks = 2048;
+    const size_t smem = (size_t)(L + 4 * 2 * L) * sizeof(double);  // L = 1024: 72 KB
+    static bool attr_set = false;
+    if (!attr_set) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&simple_features_wave_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)((kSimpleMaxL + 8 * kSimpleMaxL) * sizeof(double)));
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    hipLaunchKernelGGL(simple_features_wave_kernel, dim3((int)blocks), dim3(kSimpleThreads), smem, st,
+                       frames, n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, out);
+    return hipGetLastError();
+  }
   int64_t blocks = n_frames < 4096 ? n_frames : 4096;
   hipLaunchKernelGGL(simple_features_kernel, dim3((int)blocks), dim3(kSimpleThreads), 0, st, frames,
                      n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, out);
