@@ -15,7 +15,8 @@ dominant kernel (the MFCC kernel): its average launch duration comes from HIP
 events on the stream it is launched on, around K back-to-back launches right
 after the timed region (events between the step's kernels would idle the GPU
 ~5 us each, so the timed steps carry none); `cpu_baseline` times the oracle's vectorised NumPy restatement
-on a bounded sample on one host core (rank 0, N = 1 only).
+on a bounded sample on one host core (rank 0, N = 1 only), and
+`cpu_baseline_all_cores` the same loop on up to 16 cores, one process each.
 """
 from __future__ import annotations
 
@@ -82,6 +83,42 @@ def cpu_baseline(layers, frames_per_chunk=20000, min_seconds=10.0, max_chunks=10
             "sample": f"{n} frames ({n // frames_per_chunk} x {frames_per_chunk}-frame synthetic "
                       f"clips), oracle/vad_oracle.py vectorised NumPy (pocketfft f32 FFT, fp64 "
                       f"mel/log/DCT, fp64 features + FFN), {el:.1f} s"}
+
+
+def _cpu_chunks(args):
+    """Worker of cpu_baseline_all: the same per-chunk oracle loop on one core."""
+    n_in, frames_per_chunk, seconds, dims = args
+    from threadpoolctl import threadpool_limits
+    from oracle import vad_oracle as O
+    from vad_amd.ffn import random_layers
+    layers = random_layers(dims, seed=3)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    clip = O.synth_clip(160 * (frames_per_chunk - 1) + 401, seed=1)
+    with threadpool_limits(limits=1):
+        n, t0 = 0, time.perf_counter()
+        while n < n_in and time.perf_counter() - t0 < seconds:
+            m = O.mfcc_batch(clip, fb)
+            x = O.analyser_features_fast(m)
+            O.ffn_labels(x[:, :dims[0]], layers)
+            n += len(m)
+    return n
+
+
+def cpu_baseline_all(dims, frames_per_chunk=20000, seconds=6.0):
+    """The same oracle loop on every host core this process may use (at most
+    16, the GPU box's CPU share), one process per core (spawned: no fork of
+    the GPU process), like dataset_creator.py's multiprocessing pool."""
+    import multiprocessing as mp
+    n_proc = max(1, min(16, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(n_proc) as pool:
+        pool.map(_cpu_chunks, [(frames_per_chunk, frames_per_chunk, 60.0, dims)] * n_proc)  # warm
+        t0 = time.perf_counter()
+        n = sum(pool.map(_cpu_chunks, [(10 ** 9, frames_per_chunk, seconds, dims)] * n_proc))
+        el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "frames/s", "cores": n_proc, "kind": "port",
+            "sample": f"{n} frames on {n_proc} processes x 1 thread, same loop as cpu_baseline, "
+                      f"{el:.1f} s"}
 
 
 def main():
@@ -210,6 +247,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(layers)
+            out["cpu_baseline_all_cores"] = cpu_baseline_all(tuple(topo))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
