@@ -52,6 +52,11 @@ def main():
     out = torch.empty((F, 13), device=dev)
     t = timed(lambda: pipe.mfcc(x, out=out), a.reps)
     res["C2_mfcc_100k"] = {"frames_per_s": F / t, "us": t * 1e6}
+    # BASELINE configs[1] names 40 mel filters
+    from vad_amd.config import MfccConfig
+    pipe40 = VadPipeline(cfg=MfccConfig(n_filters=40))
+    t = timed(lambda: pipe40.mfcc(x, out=out), a.reps)
+    res["C2_mfcc_100k_40mel"] = {"frames_per_s": F / t, "us": t * 1e6}
 
     # MFCC only at 1M frames: fp32 vs int16 input
     F = 1_000_000
