@@ -140,6 +140,11 @@ size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, int64_t n_samples
 int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
                  int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                  uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
+/* The same from int16 PCM (the wav samples vad.py:37 converts with
+ * astype(float32); the conversion is exact, so the labels are identical). */
+int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const int16_t* audio,
+                     int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
+                     uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Decision-tree plan: the classifier vad.py deploys

@@ -168,6 +168,22 @@ def test_int16_input_matches_fp32(torch_cuda, fb26, nf):
     assert_mfcc_close(m16[:300].cpu().numpy(), ref)
 
 
+def test_int16_labels_match_fp32(torch_cuda, golden):
+    """VadPipeline.labels on int16 PCM (vad_mfcc_ffn_i16) == on the same
+    samples as float32 (vad_mfcc_ffn), for the FFN and the decision tree."""
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    torch = torch_cuda
+    w = golden("ffn")
+    x16 = np.clip(O.synth_clip(160 * 6000 + 241, 9), -32768, 32767).astype(np.int16)
+    a16 = torch.from_numpy(x16).cuda()
+    for clf in (FFNClassifier(layers_from(w, "ref39", 4)), _tree(golden)[1]):
+        pipe = VadPipeline(clf)
+        assert torch.equal(pipe.labels(a16), pipe.labels(a16.float()))
+    with pytest.raises(TypeError):
+        VadPipeline(FFNClassifier(layers_from(w, "ref39", 4))).labels(a16.double())
+
+
 def test_framing_edge_lengths(torch_cuda, fb26):
     from vad_amd.pipeline import VadPipeline
     pipe = VadPipeline()

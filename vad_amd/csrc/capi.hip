@@ -505,6 +505,23 @@ int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float
   return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
 }
 
+int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const int16_t* audio,
+                     int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
+                     uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream) {
+  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
+  if (f <= 5) return VAD_OK;
+  if (!audio || !labels) return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  const size_t need = vad_mfcc_ffn_workspace_bytes(plan, n_samples, frame_size, hop);
+  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
+  float* mf = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, audio, hop, frame_size, f, mf, st));
+  return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
+}
+
 int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n) {
   return n_streams * 5 * (int64_t)mfcc_n;
 }

@@ -62,12 +62,13 @@ class VadPipeline:
                                                            self.cfg.frame_size, self.cfg.hop))
 
     def labels(self, audio, out=None, stream=None):
-        """uint8 (F-5,) labels of every window of a device clip (fused path)."""
+        """uint8 (F-5,) labels of every window of a device clip (fused path);
+        float32 samples, or int16 PCM as read from a wav file (identical labels)."""
         if self.ffn is None:
             raise ValueError("pipeline has no FFN")
-        if not (isinstance(audio, torch.Tensor) and audio.is_cuda and audio.dtype == torch.float32
-                and audio.is_contiguous()):
-            raise TypeError("audio must be a contiguous float32 CUDA tensor")
+        if not (isinstance(audio, torch.Tensor) and audio.is_cuda
+                and audio.dtype in (torch.float32, torch.int16) and audio.is_contiguous()):
+            raise TypeError("audio must be a contiguous float32 or int16 CUDA tensor")
         f = self.n_frames(audio.numel())
         rows = max(f - 5, 0)
         if out is None:
@@ -79,10 +80,11 @@ class VadPipeline:
         if need and (self._ws is None or self._ws.numel() < need):
             self._ws = torch.empty((need,), dtype=torch.uint8, device=audio.device)
         ws = self._ws
-        _lib.check(_lib.lib().vad_mfcc_ffn(
+        fn = "vad_mfcc_ffn" if audio.dtype == torch.float32 else "vad_mfcc_ffn_i16"
+        _lib.check(getattr(_lib.lib(), fn)(
             self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.numel(),
             self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
-            _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), "vad_mfcc_ffn")
+            _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), fn)
         return out
 
     def process_clip(self, data):
