@@ -35,20 +35,14 @@ __device__ double block_sum(double v, double* red) {
   return r;
 }
 
+// Non-power-of-two L (e.g. 401 samples: L = 513): one workgroup per frame,
+// direct DFT (the power-of-two lengths go to simple_features_wave_kernel).
 __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     const float* __restrict__ frames, int64_t n_frames, int frame_len, int64_t frame_stride,
     int L, int pad, int band_bins, int n_bands, double* __restrict__ out) {
-  __shared__ double re[kSimpleMaxL], im[kSimpleMaxL];
-  __shared__ double twc[kSimpleMaxL / 2], tws[kSimpleMaxL / 2];  // exp(-2 pi i j / L), j < L/2
+  __shared__ double re[kSimpleMaxL];
   __shared__ double red[kSimpleThreads / 64];
   const int t = threadIdx.x;
-  const bool pow2 = (L & (L - 1)) == 0;
-  int log2L = 0;
-  while ((1 << log2L) < L) ++log2L;
-  if (pow2) {  // stage len's twiddle k / len is table entry k L / len (exact: powers of two)
-    for (int j = t; j < (L >> 1); j += kSimpleThreads) sincospi(-2.0 * (double)j / (double)L, &tws[j], &twc[j]);
-    __syncthreads();
-  }
   const int n_out = 3 + n_bands;
   for (int64_t f = blockIdx.x; f < n_frames; f += gridDim.x) {
     const float* x = frames + f * frame_stride;
@@ -65,66 +59,33 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     }
     e = block_sum(e, red);
     z = block_sum(z, red);
-    // ---- spectrum ---------------------------------------------------------
+    // ---- spectrum: X[k] = sum_n x[n] exp(-2 pi i (k n mod L) / L) -------------
     for (int i = t; i < L; i += kSimpleThreads) {
       const int s = i - pad;  // sample index (pad = 0: the first L samples)
-      const double v = (s >= 0 && s < frame_len) ? (double)x[s] : 0.0;
-      if (pow2) {
-        int r = 0;  // bit-reversed position
-        for (int b = 0; b < log2L; ++b) r |= ((i >> b) & 1) << (log2L - 1 - b);
-        re[r] = v;
-        im[r] = 0.0;
-      } else {
-        re[i] = v;
-      }
+      re[i] = (s >= 0 && s < frame_len) ? (double)x[s] : 0.0;
     }
     __syncthreads();
     double mag_sum = 0.0;
-    if (pow2) {
-      for (int len = 2; len <= L; len <<= 1) {  // iterative radix-2 DIT
-        const int half = len >> 1;
-        for (int b = t; b < (L >> 1); b += kSimpleThreads) {
-          const int grp = b / half, k = b - grp * half;
-          const int i0 = grp * len + k, i1 = i0 + half;
-          const int tw = k * (L / len);
-          const double c = twc[tw], s = tws[tw];
-          const double xr = re[i1] * c - im[i1] * s, xi = re[i1] * s + im[i1] * c;
-          const double ar = re[i0], ai = im[i0];
-          re[i0] = ar + xr;
-          im[i0] = ai + xi;
-          re[i1] = ar - xr;
-          im[i1] = ai - xi;
-        }
-        __syncthreads();
+    double mk[kSimpleMaxL / kSimpleThreads + 1];
+    int q = 0;
+    for (int k = t; k < L; k += kSimpleThreads, ++q) {
+      double ar = 0.0, ai = 0.0;
+      int kn = 0;
+      for (int n = 0; n < L; ++n) {
+        double s, c;
+        sincospi(-2.0 * (double)kn / (double)L, &s, &c);
+        ar += re[n] * c;
+        ai += re[n] * s;
+        kn += k;
+        if (kn >= L) kn -= L;
       }
-      for (int k = t; k < L; k += kSimpleThreads) {
-        const double m = sqrt(re[k] * re[k] + im[k] * im[k]);
-        mag_sum += m;
-        re[k] = m;  // magnitudes replace the real parts
-      }
-    } else {
-      // direct DFT: X[k] = sum_n x[n] exp(-2 pi i (k n mod L) / L)
-      double mk[kSimpleMaxL / kSimpleThreads + 1];
-      int q = 0;
-      for (int k = t; k < L; k += kSimpleThreads, ++q) {
-        double ar = 0.0, ai = 0.0;
-        int kn = 0;
-        for (int n = 0; n < L; ++n) {
-          double s, c;
-          sincospi(-2.0 * (double)kn / (double)L, &s, &c);
-          ar += re[n] * c;
-          ai += re[n] * s;
-          kn += k;
-          if (kn >= L) kn -= L;
-        }
-        mk[q] = sqrt(ar * ar + ai * ai);
-      }
-      __syncthreads();
-      q = 0;
-      for (int k = t; k < L; k += kSimpleThreads, ++q) {
-        re[k] = mk[q];
-        mag_sum += mk[q];
-      }
+      mk[q] = sqrt(ar * ar + ai * ai);
+    }
+    __syncthreads();
+    q = 0;
+    for (int k = t; k < L; k += kSimpleThreads, ++q) {
+      re[k] = mk[q];  // magnitudes
+      mag_sum += mk[q];
     }
     __syncthreads();
     const double mean = block_sum(mag_sum, red) / (double)L;
