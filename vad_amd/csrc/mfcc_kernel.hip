@@ -819,14 +819,11 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
   const int cap = num_cus();  // persistent, LDS-bound: one workgroup per CU
   const int grid = (int)(n_tiles < cap ? n_tiles : cap);
   const size_t smem = mfcc_smem_bytes();
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>),
-        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  static std::atomic<unsigned long long> attr_done{0};
+  const hipError_t e = ensure_dyn_lds(
+      reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>), (int)smem,
+      attr_done);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>), dim3(grid), dim3(kThreads),
                      smem, st, plan, src, stride, len, n, out);
   return hipGetLastError();

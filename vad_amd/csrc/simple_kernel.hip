@@ -218,14 +218,11 @@ hipError_t launch_simple_features(const float* frames, int64_t n_frames, int fra
     int64_t blocks = (n_frames + 3) / 4;
     if (blocks > 2048) blocks = 2048;
     const size_t smem = (size_t)(L + 4 * 2 * L) * sizeof(double);  // L = 1024: 72 KB
-    static bool attr_set = false;
-    if (!attr_set) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&simple_features_wave_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)((kSimpleMaxL + 8 * kSimpleMaxL) * sizeof(double)));
-      if (e != hipSuccess) return e;
-      attr_set = true;
-    }
+    static std::atomic<unsigned long long> attr_done{0};
+    const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simple_features_wave_kernel),
+                                        (int)((kSimpleMaxL + 8 * kSimpleMaxL) * sizeof(double)),
+                                        attr_done);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(simple_features_wave_kernel, dim3((int)blocks), dim3(kSimpleThreads), smem, st,
                        frames, n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, out);
     return hipGetLastError();

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "../../include/vad_amd.h"
 
 namespace vad {
@@ -98,6 +100,18 @@ hipError_t launch_tree_rows(const TreeNode* nodes, int n_nodes, const float* x, 
 hipError_t launch_tree_windows(const TreeNode* nodes, const TreeNodeC* cnodes, int n_nodes,
                                const float* mfcc, int64_t n_rows,
                                int mfcc_n, int mode, uint8_t* labels, hipStream_t st);
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel and device
+// (`done`: one bit per device ordinal, a static of the launch site).
+inline hipError_t ensure_dyn_lds(const void* fn, int bytes, std::atomic<unsigned long long>& done) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+  return e;
+}
 
 // NaN-keeping ReLU (numpy / Keras keep NaN; fmaxf would drop it).
 __device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }
