@@ -42,6 +42,22 @@ def test_n_frames_matches_reference_framing(golden):
     assert lib.vad_n_frames(100, 0, 160) == 0
 
 
+def test_abi_rejects_invalid_arguments():
+    """Argument checks return VAD_EINVAL before any HIP call (no GPU here)."""
+    from vad_amd import _lib
+    lib = _lib.lib()
+    E = _lib.VAD_EINVAL
+    # frame_len > 1024, hop > frame, strides shorter than the rows
+    assert lib.vad_stream_push_hop(1, 400, 1025, 1, 160, 160, 4, None) == E
+    assert lib.vad_stream_push_hop(1, 400, 400, 1, 160, 401, 4, None) == E
+    assert lib.vad_stream_push_hop(1, 399, 400, 1, 160, 160, 4, None) == E
+    assert lib.vad_stream_push_hop(None, 400, 400, None, 160, 160, 4, None) == E
+    assert lib.vad_stream_push_hop(None, 400, 400, None, 160, 160, 0, None) == _lib.VAD_OK
+    # fused clip entries without plans
+    for fn in (lib.vad_mfcc_ffn, lib.vad_mfcc_ffn_i16):
+        assert fn(None, None, None, 16000, 400, 160, 0, None, None, 0, None) == E
+
+
 def test_stream_ring_size():
     from vad_amd import _lib
     assert _lib.lib().vad_stream_ring_floats(512, 13) == 512 * 5 * 13
