@@ -82,6 +82,22 @@ def main():
         t = timed(step, max(10, a.reps // 2))
         res[f"C3_mfcc_ffn_{name}"] = {"frames_per_s": F / t, "us": t * 1e6}
 
+    # PCIe-inclusive: the clip in pinned host memory (fp32, and int16 PCM at
+    # half the bytes) -> H2D copy -> fused MFCC + features + FFN -> labels
+    clf = ffn_mod.FFNClassifier(ffn_mod.random_layers(ffn_mod.TOPOLOGY_BL13, seed=3))
+    p = VadPipeline(ffn=clf)
+    lab = torch.empty((F - 5,), dtype=torch.uint8, device=dev)
+    for name, src in (("fp32", x), ("int16", x16)):
+        host = src.cpu().pin_memory()
+        dbuf = torch.empty_like(src)
+
+        def e2e():
+            dbuf.copy_(host, non_blocking=True)
+            p.labels(dbuf, out=lab)
+        t = timed(e2e, max(10, a.reps // 2), warm=10)
+        res[f"C3_host_clip_to_labels_{name}"] = {"frames_per_s": F / t, "us": t * 1e6,
+                                                 "host_bytes": host.numel() * host.element_size()}
+
     # MFCC + decision tree (the classifier vad.py deploys), fixture tree
     from vad_amd.tree import TreeClassifier
     gt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests",
