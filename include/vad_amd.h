@@ -133,9 +133,13 @@ int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t*
 /* Clip path: framing + MFCC + features + FFN (dataset_creator/process_file
  * framing, file_processing.py:38-70, with the analyser's classifier call,
  * sklearn_analyser.py:71).  labels[i] for windows i < n_frames-5 of the clip.
- * `workspace` (device, >= vad_mfcc_ffn_workspace_bytes()) holds intermediate
- * MFCCs when the build does not keep them on chip; 0 bytes when fused. */
-size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, int64_t n_samples,
+ * One fused kernel (MFCC rows stay on chip, no workspace) for the reference
+ * framing (frame 400, hop 160), the compiled 26-filter bank, a split-f16
+ * FFN topology (39-64-32-16-3 or 13-64-64-N) and pair-aligned audio (8 B for
+ * fp32, 4 B for int16: every torch allocation is); any other configuration
+ * runs the MFCC and window kernels through `workspace` (device, >=
+ * vad_mfcc_ffn_workspace_bytes(), which is 0 when the fused kernel applies). */
+size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int64_t n_samples,
                                     int32_t frame_size, int32_t hop);
 int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
                  int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
@@ -145,6 +149,12 @@ int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float
 int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const int16_t* audio,
                      int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                      uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
+/* The two-kernel form (MFCC rows through the workspace, always required here)
+ * of vad_mfcc_ffn (in_bytes 4) / vad_mfcc_ffn_i16 (in_bytes 2): the A/B
+ * baseline of the fused kernel, identical labels. */
+int vad_mfcc_ffn_unfused(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int32_t in_bytes,
+                         int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Decision-tree plan: the classifier vad.py deploys

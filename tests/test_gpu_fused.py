@@ -1,0 +1,86 @@
+"""The fused clip kernel (vad_mfcc_ffn: MFCC -> window features -> FFN in one
+launch, MFCC rows kept on chip) against the two-kernel form and the oracle.
+
+Labels of the fused and the two-kernel path must be identical bit for bit
+(same MFCC arithmetic, same features, same split-f16 forward): clip lengths
+around every workgroup / tile / halo boundary, both specialised topologies and
+a 3-class bl13, fp32 and int16 input, analyser and offline features.
+"""
+import numpy as np
+import pytest
+
+from oracle import vad_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOPOS = ((13, 64, 64, 2), (39, 64, 32, 16, 3), (13, 64, 64, 3))
+# F frames: a single partial tile, the first tile-edge windows, 256-workgroup
+# splits with 1..2 tiles each, uneven splits, and multi-tile runs
+FRAMES = (6, 7, 8, 64, 68, 69, 70, 133, 1000, 16_389, 16_389 + 257, 65_541, 100_003)
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+def _pipe(topo, mode="analyser"):
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    return VadPipeline(FFNClassifier(random_layers(topo, seed=3)), mode=mode)
+
+
+@pytest.mark.parametrize("topo", TOPOS)
+def test_fused_equals_two_kernel(torch_cuda, topo):
+    torch = torch_cuda
+    clip = O.synth_clip(O.samples_for_frames(max(FRAMES)), seed=21)
+    clip[160 * 5000:160 * 5100] = 0.0  # digital silence: NaN windows -> class 0
+    a32 = torch.from_numpy(clip).cuda()
+    a16 = a32.round().clamp(-32768, 32767).to(torch.int16)
+    for mode in ("analyser", "offline"):
+        pipe = _pipe(topo, mode)
+        assert pipe.workspace_bytes(a32.numel()) == 0  # the fused kernel applies
+        for F in FRAMES:
+            n = O.samples_for_frames(F)
+            for a in (a32[:n], a16[:n]):
+                got = pipe.labels(a)
+                want = pipe.labels_unfused(a)
+                assert got.numel() == F - 5
+                assert torch.equal(got, want), (topo, mode, F, a.dtype,
+                                                int((got != want).sum()))
+
+
+def test_fused_unaligned_and_fallbacks(torch_cuda):
+    """An audio view starting one sample in (not pair-aligned) and a 40-filter
+    plan run the two-kernel path through a workspace: same labels."""
+    torch = torch_cuda
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 3000
+    clip = O.synth_clip(O.samples_for_frames(F) + 1, seed=22)
+    base = torch.from_numpy(clip).cuda()
+    pipe = _pipe(TOPOS[0])
+    view = base[1:]  # contiguous, 4-byte but not 8-byte aligned
+    assert view.data_ptr() % 8 == 4
+    assert pipe.workspace_bytes(view.numel(), view) > 0
+    ref = pipe.labels_unfused(view.clone())
+    assert torch.equal(pipe.labels(view), ref)
+    p40 = VadPipeline(FFNClassifier(random_layers(TOPOS[0], seed=3)),
+                      cfg=MfccConfig(n_filters=40))
+    assert p40.workspace_bytes(base.numel()) > 0
+    assert torch.equal(p40.labels(base), p40.labels_unfused(base))
+
+
+def test_fused_out_checks(torch_cuda):
+    torch = torch_cuda
+    pipe = _pipe(TOPOS[0])
+    a = torch.from_numpy(O.synth_clip(O.samples_for_frames(500), seed=23)).cuda()
+    with pytest.raises(ValueError):
+        pipe.labels(a, out=torch.empty(10, dtype=torch.uint8, device="cuda"))
+    with pytest.raises(TypeError):
+        pipe.labels(a, out=torch.empty(495, dtype=torch.int32, device="cuda"))
+    out = torch.empty(495, dtype=torch.uint8, device="cuda")
+    assert pipe.labels(a, out=out) is out

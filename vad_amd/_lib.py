@@ -52,11 +52,13 @@ SIGNATURES = {
     "vad_scale_workspace_bytes": (c_sz, []),
     "vad_scale_features": (c_int, [c_vp, c_i64, c_i32, c_vp, c_sz, c_vp]),
     "vad_format_csv_rows": (c_i64, [c_vp, c_i64, c_i32, ctypes.c_double, c_vp, c_i64]),
-    "vad_mfcc_ffn_workspace_bytes": (c_sz, [c_vp, c_i64, c_i32, c_i32]),
+    "vad_mfcc_ffn_workspace_bytes": (c_sz, [c_vp, c_vp, c_i64, c_i32, c_i32]),
     "vad_mfcc_ffn": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_sz,
                              c_vp]),
     "vad_mfcc_ffn_i16": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_sz,
                                  c_vp]),
+    "vad_mfcc_ffn_unfused": (c_int, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp,
+                                     c_sz, c_vp]),
     "vad_stream_ring_floats": (c_i64, [c_i64, c_i32]),
     "vad_stream_push_hop": (c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,

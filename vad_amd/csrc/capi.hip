@@ -481,45 +481,63 @@ int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t*
   return (int)launch_ffn(ffn->net, 1, x, n, 0, 0, labels, (hipStream_t)stream);
 }
 
-size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, int64_t n_samples,
+size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int64_t n_samples,
                                     int32_t frame_size, int32_t hop) {
-  if (!plan) return 0;
+  if (!plan || !ffn) return 0;
+  // the fused kernel keeps the MFCC rows on chip (pair-aligned audio assumed:
+  // any torch allocation is)
+  if (mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, nullptr, 4)) return 0;
   const int64_t f = vad_n_frames(n_samples, frame_size, hop);
   return (size_t)f * plan->host.mfcc_n * sizeof(float);
+}
+
+// Shared body of vad_mfcc_ffn / vad_mfcc_ffn_i16: the fused kernel when the
+// configuration allows it, else MFCC rows through the workspace and the
+// window kernel.
+static int mfcc_ffn_entry(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int tin_bytes,
+                          int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
+                          void* workspace, size_t workspace_bytes, void* stream, bool allow_fused = true) {
+  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1) ||
+      (tin_bytes != 2 && tin_bytes != 4))
+    return VAD_EINVAL;
+  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
+  if (f <= 5) return VAD_OK;
+  if (!audio || !labels) return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (allow_fused && mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, audio, tin_bytes))
+    return (int)launch_mfcc_ffn(plan->dev, ffn->net, audio, tin_bytes, f, mode, labels, st);
+  const size_t need = (size_t)f * plan->host.mfcc_n * sizeof(float);
+  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
+  float* mf = (float*)workspace;
+  if (tin_bytes == 2)
+    VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, (const int16_t*)audio, hop, frame_size, f, mf, st));
+  else
+    VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, (const float*)audio, hop, frame_size, f, mf, st));
+  return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
 }
 
 int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
                  int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                  uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream) {
-  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1))
-    return VAD_EINVAL;
-  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
-  if (f <= 5) return VAD_OK;
-  if (!audio || !labels) return VAD_EINVAL;
-  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
-  const size_t need = vad_mfcc_ffn_workspace_bytes(plan, n_samples, frame_size, hop);
-  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
-  float* mf = (float*)workspace;
-  hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, audio, hop, frame_size, f, mf, st));
-  return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
+  return mfcc_ffn_entry(plan, ffn, audio, 4, n_samples, frame_size, hop, mode, labels, workspace,
+                        workspace_bytes, stream);
 }
 
 int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const int16_t* audio,
                      int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                      uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream) {
-  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1))
-    return VAD_EINVAL;
-  const int64_t f = vad_n_frames(n_samples, frame_size, hop);
-  if (f <= 5) return VAD_OK;
-  if (!audio || !labels) return VAD_EINVAL;
-  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
-  const size_t need = vad_mfcc_ffn_workspace_bytes(plan, n_samples, frame_size, hop);
-  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
-  float* mf = (float*)workspace;
-  hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, audio, hop, frame_size, f, mf, st));
-  return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
+  return mfcc_ffn_entry(plan, ffn, audio, 2, n_samples, frame_size, hop, mode, labels, workspace,
+                        workspace_bytes, stream);
+}
+
+/* Two-kernel form of vad_mfcc_ffn (MFCC rows through the caller's workspace,
+ * then the window kernel), kept for A/B measurement and tests. */
+int vad_mfcc_ffn_unfused(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int32_t in_bytes,
+                         int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
+                         void* workspace, size_t workspace_bytes, void* stream) {
+  return mfcc_ffn_entry(plan, ffn, audio, in_bytes, n_samples, frame_size, hop, mode, labels, workspace,
+                        workspace_bytes, stream, false);
 }
 
 int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n) {

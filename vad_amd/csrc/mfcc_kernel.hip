@@ -25,13 +25,12 @@
 //            lifter x DCT of the log-mel rows, stored to the MFCC rows.  It
 //            runs deferred, in the next tile after phase 1, on the waves that
 //            finish their FFT first -- two barriers per tile.
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "vad_common.h"
 #include "fft_pk.h"
 #include "mel_tables.h"
+#include "ffn_dev.h"
 
 namespace vad {
 
@@ -51,6 +50,9 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 // the conversion is exact, so both inputs give identical spectra).
 #ifndef VAD_NO_STORE
 #define VAD_NO_STORE 0  // diagnostic builds only: MFCC results are not written
+#endif
+#ifndef VAD_DIAG_BUILD
+#define VAD_DIAG_BUILD 0  // 0 in the shipped library: no diagnostic kernel is instantiated
 #endif
 #ifndef VAD_NT_LOADS
 #define VAD_NT_LOADS 0
@@ -171,6 +173,60 @@ __device__ __forceinline__ void lane_consts(const MfccDev* __restrict__ plan, in
   for (int k1 = 0; k1 < 16; ++k1) L.twa[k1] = ta[j * 16 + k1];
 #pragma unroll
   for (int m = 0; m < 8; ++m) L.twb[m] = tb[L.e0 + 32 * m + (m >= 4 ? L.off4 : 0)];
+}
+
+// Per-lane twiddles staged in LDS (the fused kernel: its VGPRs go to the FFN
+// between tiles): row j of twa holds W256^(j k1), k1 = 0..15, at a stride of
+// 18 complex, row j of twb lane j's eight W512^kE(m) at a stride of 10 --
+// 16-B aligned rows whose ds_read_b128 lane groups hit disjoint banks (the
+// four 16-lane groups of a wave read the same rows: broadcasts).
+constexpr int kTwaStride = 18, kTwbStride = 10;
+constexpr size_t kTwLdsBytes = (size_t)16 * (kTwaStride + kTwbStride) * sizeof(v2f);
+
+__device__ __forceinline__ void lane_ints(int j, LaneConsts& L) {
+  if (j < 14) {
+    const int p = (j >> 1) + 1;
+    L.cE = (j & 1) ? 16 - p : p;
+    L.cO = 16 - L.cE;
+  } else {
+    L.cE = L.cO = (j == 14) ? 0 : 8;
+  }
+  L.col0 = (j == 14);
+  L.e0 = L.cE;
+  L.off4 = L.col0 ? 16 : 0;
+  L.kO0 = L.col0 ? 128 : 256 - L.cE;
+}
+
+__device__ __forceinline__ void stage_twiddles(const MfccDev* __restrict__ plan, v2f* __restrict__ tw, int tid,
+                                               int nthreads) {
+  for (int i = tid; i < 16 * 16; i += nthreads) {
+    const int j = i >> 4, k = i & 15;
+    tw[j * kTwaStride + k] = reinterpret_cast<const v2f*>(plan->tw_a)[i];
+    if (k < 8) {
+      LaneConsts L;
+      lane_ints(j, L);
+      tw[16 * kTwaStride + j * kTwbStride + k] =
+          reinterpret_cast<const v2f*>(plan->tw_b)[L.e0 + 32 * k + (k >= 4 ? L.off4 : 0)];
+    }
+  }
+}
+
+__device__ __forceinline__ void lane_consts_lds(const v2f* __restrict__ tw, int j, LaneConsts& L) {
+  lane_ints(j, L);
+  const v4f* a = reinterpret_cast<const v4f*>(__builtin_assume_aligned(tw + j * kTwaStride, 16));
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const v4f t = a[q];
+    L.twa[2 * q] = t.xy;
+    L.twa[2 * q + 1] = t.zw;
+  }
+  const v4f* b = reinterpret_cast<const v4f*>(__builtin_assume_aligned(tw + 16 * kTwaStride + j * kTwbStride, 16));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const v4f t = b[q];
+    L.twb[2 * q] = t.xy;
+    L.twb[2 * q + 1] = t.zw;
+  }
 }
 
 // Phase 1 for one frame of a 16-lane group, in three steps so that a wave
@@ -502,7 +558,9 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// DIAG 5/6 (diagnostic builds only, VAD_DIAG env): timestamps, outputs wrong.
+// DIAG (diagnostic library builds only: `python -m vad_amd.build --variant NAME
+// -DVAD_DIAG_BUILD=n`, never the shipped libvad_amd.so): 5/6 timestamps, 7 an
+// L2-resident source, 9 per-workgroup stamps, 10 phase 1 only -- outputs wrong.
 // HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
@@ -815,6 +873,209 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused clip path: framing -> MFCC -> 5-frame window features -> FFN ->
+// labels (mfcc.py:59-78, sklearn_analyser.py:52-71 / file_processing.py:51-66,
+// ffn_trainer.py:106-116); the MFCC rows never leave the CU.
+//   Workgroup b owns windows [wb, we) (window i = frames i .. i+4) and runs
+//   frames [wb, we + 4) in 64-frame tiles of its own: the 4-frame halo is
+//   recomputed by the neighbour (4 frames per workgroup, 0.1 % at 1M frames).
+//   Per tile t (two barriers, as in mfcc_kernel's paired-frame loop):
+//     phase 1     all waves: FFT of tile t -> power rows P;
+//     waves 0..3  lifter x DCT of tile t-1's log-mel rows -> MFCC ring buffer
+//                 (t-1) & 1, rows 4..67 (rows 0..3: tile t-2's last four,
+//                 copied); then the FFN of tile t-2's 64 windows from buffer
+//                 t & 1, wave w taking windows 16 w .. 16 w + 15: features
+//                 into its own (now idle) FFT scratch slice, split-f16 MFMA
+//                 forward with the weight fragments read from L1 / L2 (the
+//                 VGPRs and LDS are the FFT's), label store;
+//     barrier;  phase 2a (mel + log10 of tile t);  barrier.
+//   Buffer (t-2) & 1 was completed before tile t-1's first barrier and is
+//   next written in tile t+1, after tile t's second barrier.
+// ---------------------------------------------------------------------------
+// The compiler may not treat loads through a laundered pointer as loop
+// invariant: the FFN's weight fragments and the FFT's per-lane twiddles are
+// re-read where they are used instead of being hoisted out of the tile loop
+// (where ~170 VGPRs of them would stay live through the FFT and spill).
+template <class Ptr>
+__device__ __forceinline__ Ptr launder(Ptr p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
+#ifndef VAD_FUSED_DIAG
+#define VAD_FUSED_DIAG 0  // diagnostic builds only: 1 zero weight fragments (no loads), 2 no FFN,
+                          // 3 features only, 5 no FFN and the twiddles kept in VGPRs
+#endif
+
+constexpr int kRingRows = kTile + 4;
+constexpr int kRingFloats = kRingRows * 13;
+
+// compact per-lane-group tables of the FFN's bias and VALU output-layer
+// slots (LdsSlots): 4 floats per slot, at most 36 bias + 68 output slots (bl13, 4 classes)
+constexpr int kSlotTableFloats = 4 * 112;
+
+template <int SPEC>
+constexpr size_t fused_smem_bytes() {
+  return kPBytes + kScrBytes + (size_t)kTile * lm_stride<SPEC>() * sizeof(float) +
+         2 * (size_t)kRingFloats * sizeof(float) + kSlotTableFloats * sizeof(float) + kTwLdsBytes;
+}
+
+template <typename TIN, int SPEC, int MODE, int KS0, int T1, int T2, int T3, int T4, int NC>
+__global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __restrict__ plan, FfnDev net,
+                                                               const TIN* __restrict__ src, int64_t n_frames,
+                                                               uint8_t* __restrict__ labels) {
+  using T = std::conditional_t<SPEC == 1, Mel26, Mel40>;
+  static_assert(T::NC == 13, "the wave tile reads 13 coefficients per row");
+  constexpr int LEN = 400, HOPC = 5, NZ = 13, NB = NZ + HOPC, MN = 13;
+  using TP = Topo<KS0, T1, T2, T3, T4, NC>;
+  using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+  constexpr int IN = KS0 == 4 ? MN : 3 * MN;  // network inputs (features 0 .. IN-1)
+  constexpr int XS = 32 * HP::K0 + 4;         // floats per feature row: 16-B aligned
+  static_assert((kWTile * XS + kWTile) * 4 <= 4 * kGroupScratch * (int)sizeof(v2f),
+                "a wave's features fit its FFT scratch slice");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* P = reinterpret_cast<float*>(smem);                      // [64][260] power rows
+  v2f* scr = reinterpret_cast<v2f*>(smem + kPBytes);              // FFT transposes
+  float* lm = reinterpret_cast<float*>(smem + kPBytes + kScrBytes);  // [64][LMS] log-mel
+  float* ring = lm + kTile * lm_stride<SPEC>();                   // 2 x [68][13] MFCC rows
+  float* stbl = ring + 2 * kRingFloats;                           // FFN bias / output slots
+  v2f* tw = reinterpret_cast<v2f*>(stbl + kSlotTableFloats);      // per-lane FFT twiddles
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = tid >> 4;
+  const int j = tid & 15;
+  const int64_t n_win = n_frames - 5;
+  const int64_t wb = n_win * blockIdx.x / gridDim.x;
+  const int64_t we = n_win * (blockIdx.x + 1) / gridDim.x;
+  if (wb >= we) return;  // workgroup-uniform
+  const int64_t fs = wb;  // first frame of tile 0
+  const int n_t = (int)((we + 4 - fs + kTile - 1) / kTile);
+
+  v2f* gscr = scr + grp * kGroupScratch;
+  LaneConsts L;
+  stage_twiddles(plan, tw, tid, kThreads);
+  const int64_t flast = n_frames - 1;
+  auto pair_base = [&](int t, int& lim) __attribute__((always_inline)) {
+    const int64_t F = fs + (int64_t)t * kTile + 2 * grp;
+    lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
+    return src + (F < flast ? F : flast) * (32 * HOPC);
+  };
+  // bias and VALU output-layer slots: one value per lane group -> LDS table
+  {
+    constexpr int NS = TP::NB + TP::NV + TP::NVB;
+    static_assert(4 * NS <= kSlotTableFloats, "slot table");
+    for (int i = tid; i < 4 * NS; i += kThreads) {
+      const int sl = i >> 2, gg = i & 3;
+      // slots after the biases: the VALU layer's (host order: 4 classes, then biases)
+      const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
+                                     : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
+                                                                                  : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
+      stbl[i] = net.frag[src_sl * 64 + 16 * gg];
+    }
+  }
+  float* X = reinterpret_cast<float*>(scr + 4 * wave * kGroupScratch);  // waves 0..3: own slice
+  int* FL = reinterpret_cast<int*>(X + kWTile * XS);
+  const int g4 = lane >> 4;
+
+  // lifter x DCT of tile tt's log-mel rows (one frame per lane, coefficients
+  // wave + 4 i) into ring buffer tt & 1, plus the carried rows
+  auto dct_to_ring = [&](int tt) __attribute__((always_inline)) {
+    float acc[4];
+    dct_dispatch<T>(wave, lm + lane * lm_stride<SPEC>(), acc);
+    float* M = ring + (tt & 1) * kRingFloats;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (wave + kDctGroups * i < MN) M[(4 + lane) * MN + wave + kDctGroups * i] = acc[i];
+    if (wave == 0 && lane < 4 * MN) M[lane] = ring[((tt + 1) & 1) * kRingFloats + kTile * MN + lane];
+  };
+  // windows 16 wave .. 16 wave + 15 of ring buffer tt & 1 (row r = frame
+  // fs + 64 tt - 4 + r; window 16 wave + jw starts at that row)
+  // windows of buffer tt & 1 after the DCT of tile td (td < 0: none); the
+  // split-f16 weight fragments of every layer are requested at once before
+  // the DCT (one L2 round trip, covered by the DCT and the features)
+  auto dct_ffn_tile = [&](int td, int tt) __attribute__((always_inline)) {
+    u4 frh[HP::NS][2];
+    if constexpr (VAD_FUSED_DIAG == 1) {
+#pragma unroll
+      for (int sl = 0; sl < HP::NS; ++sl) frh[sl][0] = frh[sl][1] = (u4){0u, 0u, 0u, 0u};
+    } else {
+      load_fragh<HP>(reinterpret_cast<const uint32_t*>(launder(net.fragh)), lane, frh);
+    }
+    if (td >= 0) dct_to_ring(td);
+    if constexpr (VAD_FUSED_DIAG == 2 || VAD_FUSED_DIAG == 5) return;
+    const LdsSlots fb{stbl + g4};
+    const LdsSlots fv{stbl + 4 * TP::NB + g4};
+    const float* R = ring + (tt & 1) * kRingFloats + 16 * wave * MN;
+    wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
+    if constexpr (VAD_FUSED_DIAG == 3) {
+      if (lane < 16) labels[fs + 16 * wave + lane] = (uint8_t)X[lane * XS + 3];
+      return;
+    }
+    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true>(
+        X, FL, lane, FragRegs{frh}, fb, fv, net.n_classes);
+    const int64_t i = fs + (int64_t)tt * kTile - 4 + 16 * wave + (lane & 15);
+    if (lane < 16 && i >= wb && i < we) labels[i] = (uint8_t)lab;
+  };
+
+  __syncthreads();  // twiddles and slot tables staged
+  v2f buf[NB];
+  {
+    int lim;
+    const TIN* b0 = pair_base(0, lim);
+    load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  for (int t = 0; t < n_t; ++t) {
+    // twiddles from LDS each tile: dead (and their VGPRs free for the FFN)
+    // between phase 1 and the next tile
+    if (VAD_FUSED_DIAG != 5 || t == 0) lane_consts_lds(tw, j, L);
+    float* prow_a = P + (2 * grp) * kPStride;
+    float* prow_b = P + (2 * grp + 1) * kPStride;
+    int lim;
+    const TIN* nb = pair_base(t + 1, lim);
+    v2f u[16], col[32];
+    VAD_MILESTONE(3);
+    stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+    __builtin_amdgcn_sched_barrier(0);
+    load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    store_a(u, gscr, j);
+    read_b(L, gscr, col);
+    __builtin_amdgcn_sched_barrier(0);
+    VAD_MILESTONE(2);
+    stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
+    __builtin_amdgcn_sched_barrier(0);
+    load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    VAD_MILESTONE(1);
+    finish_b<false>(L, col, prow_a);
+    __builtin_amdgcn_sched_barrier(0);
+    load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    VAD_MILESTONE(0);
+    store_a(u, gscr, j);
+    read_b(L, gscr, col);
+    finish_b<false>(L, col, prow_b);
+    __builtin_amdgcn_sched_barrier(0);
+    if (wave < kDctGroups) {
+      if (t >= 2) dct_ffn_tile(t - 1, t - 2);
+      else if (t == 1) dct_to_ring(0);
+    }
+    lds_barrier();  // P complete; log-mel rows consumed; ring buffer (t-1) & 1 complete
+    phase2a<SPEC>(plan, P, lm, wave, lane);
+    lds_barrier();  // log-mel rows complete; P and the FFT scratch free
+  }
+  if (wave < kDctGroups) {
+    if (n_t >= 2) dct_ffn_tile(n_t - 1, n_t - 2);
+    else dct_to_ring(n_t - 1);
+  }
+  lds_barrier();
+  if (wave < kDctGroups) dct_ffn_tile(-1, n_t - 1);
+}
+
 size_t mfcc_smem_bytes() { return kPBytes + kScrBytes + kLmBytes; }  // 157,696 B
 
 static int num_cus() {
@@ -854,18 +1115,13 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
                     ((stride & 1) == 0) && ((used & 1) == 0);
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
-      static const int diag = getenv("VAD_DIAG") ? atoi(getenv("VAD_DIAG")) : 0;
-      if (diag == 5 && stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 5, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 9 && stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 9, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 7 && stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 7, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 10 && stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 10, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 5 || diag == 8) return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st);
-      if (diag == 6) return launch_t<TIN, MODE, 13, true, 400, 1, 6>(plan, src, stride, len, n, out, st);
-      if (diag == 7) return launch_t<TIN, MODE, 13, true, 400, 1, 7>(plan, src, stride, len, n, out, st);
+      if constexpr (VAD_DIAG_BUILD != 0) {  // diagnostic library builds only (outputs wrong)
+        constexpr int D = VAD_DIAG_BUILD == 8 ? 5 : VAD_DIAG_BUILD;
+        constexpr bool kPairedDiag = D == 5 || D == 7 || D == 9 || D == 10;
+        if (kPairedDiag && VAD_DIAG_BUILD != 8 && stride == 160 && kPairFrames)
+          return launch_t<TIN, MODE, 13, true, 400, 1, D, 5>(plan, src, stride, len, n, out, st);
+        return launch_t<TIN, MODE, 13, true, 400, 1, D == 9 || D == 10 ? 0 : D>(plan, src, stride, len, n, out, st);
+      }
       if (stride == 160 && kPairFrames)  // the reference hop (config.py:22)
         return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
@@ -905,6 +1161,56 @@ hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_
   if (n <= 0) return hipSuccess;
   if (mode == kAudioToSpec) return launch_m<int16_t, kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
   return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
+}
+
+// Fused clip entry (vad_mfcc_ffn): the reference framing (400 / 160), the
+// compiled 26-filter bank and a split-f16 topology; false -> the caller runs
+// the two-kernel path through a workspace.
+bool mfcc_ffn_fusable(int spec, const FfnDev& net, int frame_size, int hop, const void* audio, int tin_bytes) {
+  if (!kPairFrames || spec != 1 || frame_size != 400 || hop != 160 || !net.fragh) return false;
+  if (reinterpret_cast<uintptr_t>(audio) % (2 * tin_bytes) != 0) return false;  // sample-pair loads
+  const int* t = net.tiles;
+  const bool ref39 = net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1;
+  const bool bl13 = net.n_layers == 3 && net.ks0 == 4 && t[0] == 4 && t[1] == 4 && t[2] == 1;
+  return ref39 || bl13;
+}
+
+template <typename TIN, int MODE, int KS0, int T1, int T2, int T3, int T4, int NC>
+static hipError_t launch_fused_t(const MfccDev* plan, const FfnDev& net, const TIN* src, int64_t n_frames,
+                                 uint8_t* labels, hipStream_t st) {
+  const int64_t n_win = n_frames - 5;
+  const int64_t want = (n_win + kTile - 1) / kTile;
+  const int cap = num_cus();  // persistent, LDS-bound: one workgroup per CU
+  const int grid = (int)(want < cap ? want : cap);
+  constexpr size_t smem = fused_smem_bytes<1>();
+  static std::atomic<unsigned long long> attr_done{0};
+  const hipError_t e = ensure_dyn_lds(
+      reinterpret_cast<const void*>(&mfcc_ffn_kernel<TIN, 1, MODE, KS0, T1, T2, T3, T4, NC>), (int)smem, attr_done);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((mfcc_ffn_kernel<TIN, 1, MODE, KS0, T1, T2, T3, T4, NC>), dim3(grid), dim3(kThreads), smem, st,
+                     plan, net, src, n_frames, labels);
+  return hipGetLastError();
+}
+
+template <typename TIN, int MODE>
+static hipError_t launch_fused_m(const MfccDev* plan, const FfnDev& net, const TIN* src, int64_t n_frames,
+                                 uint8_t* labels, hipStream_t st) {
+  if (net.ks0 == 10) return launch_fused_t<TIN, MODE, 10, 4, 2, 1, 1, 4>(plan, net, src, n_frames, labels, st);
+  if (net.n_classes <= 2) return launch_fused_t<TIN, MODE, 4, 4, 4, 1, 0, 2>(plan, net, src, n_frames, labels, st);
+  return launch_fused_t<TIN, MODE, 4, 4, 4, 1, 0, 4>(plan, net, src, n_frames, labels, st);
+}
+
+hipError_t launch_mfcc_ffn(const MfccDev* plan, const FfnDev& net, const void* audio, int tin_bytes,
+                           int64_t n_frames, int mode, uint8_t* labels, hipStream_t st) {
+  if (n_frames <= 5) return hipSuccess;
+  if (tin_bytes == 2) {
+    const int16_t* a = static_cast<const int16_t*>(audio);
+    return mode == VAD_FEAT_OFFLINE ? launch_fused_m<int16_t, VAD_FEAT_OFFLINE>(plan, net, a, n_frames, labels, st)
+                                    : launch_fused_m<int16_t, VAD_FEAT_ANALYSER>(plan, net, a, n_frames, labels, st);
+  }
+  const float* a = static_cast<const float*>(audio);
+  return mode == VAD_FEAT_OFFLINE ? launch_fused_m<float, VAD_FEAT_OFFLINE>(plan, net, a, n_frames, labels, st)
+                                  : launch_fused_m<float, VAD_FEAT_ANALYSER>(plan, net, a, n_frames, labels, st);
 }
 
 }  // namespace vad

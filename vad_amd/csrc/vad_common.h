@@ -80,6 +80,9 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src
                        int len, int64_t n, float* out, hipStream_t st);
 hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_t* src,
                            int64_t stride, int len, int64_t n, float* out, hipStream_t st);
+bool mfcc_ffn_fusable(int spec, const FfnDev& net, int frame_size, int hop, const void* audio, int tin_bytes);
+hipError_t launch_mfcc_ffn(const MfccDev* plan, const FfnDev& net, const void* audio, int tin_bytes,
+                           int64_t n_frames, int mode, uint8_t* labels, hipStream_t st);
 hipError_t launch_ffn(const FfnDev& net, int src, const float* in, int64_t n_rows, int mfcc_n,
                       int mode, uint8_t* labels, hipStream_t st);
 hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring, int* count,

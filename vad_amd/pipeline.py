@@ -5,7 +5,8 @@ process_file) -> split_into_frames (file_processing.py:80-103) -> per-frame
 get_mfcc -> 5-frame feature window (file_processing.py:40-70), with the
 analyser's classifier applied to every window (sklearn_analyser.py:52-71).
 Here a whole clip resident in HBM is framed, transformed and classified by
-two HIP kernels; the host only sizes buffers.
+one fused HIP kernel (the MFCC rows never leave the CU); the host only sizes
+buffers.
 """
 from __future__ import annotations
 
@@ -15,7 +16,7 @@ import torch
 from . import _lib
 from .config import MfccConfig
 from .ffn import FFNClassifier
-from .plan import MfccPlan, n_frames, window_features
+from .plan import MfccPlan, check_out, n_frames, window_features
 
 
 def split_into_frames(data, frame_size, step, transcription_path=None, frame_rate=None):
@@ -43,7 +44,7 @@ class VadPipeline:
             ffn = FFNClassifier(ffn)
         self.ffn = ffn
         self.mode = _lib.FEAT_ANALYSER if mode == "analyser" else _lib.FEAT_OFFLINE
-        self._ws = None
+        self._ws = {}  # (device index, stream) -> workspace
 
     def n_frames(self, n_samples):
         return n_frames(n_samples, self.cfg.frame_size, self.cfg.hop)
@@ -57,34 +58,71 @@ class VadPipeline:
         m = self.mfcc(audio, stream=stream)
         return window_features(m, self.mode if mode is None else mode, stream=stream)
 
-    def workspace_bytes(self, n_samples):
-        return int(_lib.lib().vad_mfcc_ffn_workspace_bytes(self.plan.handle, int(n_samples),
-                                                           self.cfg.frame_size, self.cfg.hop))
+    def workspace_bytes(self, n_samples, audio=None):
+        """Device bytes vad_mfcc_ffn needs: 0 on the fused kernel (reference
+        framing, 26 filters, split-f16 FFN, pair-aligned audio), else the
+        (F, n_mfcc) fp32 MFCC rows of the two-kernel path."""
+        need = int(_lib.lib().vad_mfcc_ffn_workspace_bytes(
+            self.plan.handle, self.ffn.plan.handle, int(n_samples), self.cfg.frame_size, self.cfg.hop))
+        if need == 0 and audio is not None and audio.data_ptr() % (2 * audio.element_size()):
+            need = self.n_frames(n_samples) * self.plan.mfcc_n * 4  # unaligned: two kernels
+        return need
 
-    def labels(self, audio, out=None, stream=None):
-        """uint8 (F-5,) labels of every window of a device clip (fused path);
-        float32 samples, or int16 PCM as read from a wav file (identical labels)."""
+    def _workspace(self, need, device, stream):
+        """Cached workspace per (device, stream): a buffer is never shared by
+        work on two streams or handed to a kernel on another device."""
+        if need == 0:
+            return None
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        key = (device.index, s.cuda_stream)
+        ws = self._ws.get(key)
+        if ws is None or ws.numel() < need:
+            with torch.cuda.stream(s):
+                ws = torch.empty((need,), dtype=torch.uint8, device=device)
+            self._ws[key] = ws
+        return ws
+
+    def _check_labels_call(self, audio, out):
         if self.ffn is None:
             raise ValueError("pipeline has no FFN")
         if not (isinstance(audio, torch.Tensor) and audio.is_cuda
                 and audio.dtype in (torch.float32, torch.int16) and audio.is_contiguous()):
             raise TypeError("audio must be a contiguous float32 or int16 CUDA tensor")
-        f = self.n_frames(audio.numel())
-        rows = max(f - 5, 0)
+        rows = max(self.n_frames(audio.numel()) - 5, 0)
         if out is None:
             out = torch.empty((rows,), dtype=torch.uint8, device=audio.device)
+        else:
+            check_out(out, (rows,), torch.uint8, audio.device, "out")
+        return out
+
+    def labels(self, audio, out=None, stream=None):
+        """uint8 (F-5,) labels of every window of a device clip -- one fused
+        MFCC + features + FFN kernel (vad_mfcc_ffn); float32 samples, or int16
+        PCM as read from a wav file (identical labels)."""
+        out = self._check_labels_call(audio, out)
         if not isinstance(self.ffn, FFNClassifier):  # decision tree: MFCC, then windows
             return self.ffn.window_labels(self.mfcc(audio, stream=stream), self.mode, out=out,
                                           stream=stream)
-        need = self.workspace_bytes(audio.numel())
-        if need and (self._ws is None or self._ws.numel() < need):
-            self._ws = torch.empty((need,), dtype=torch.uint8, device=audio.device)
-        ws = self._ws
+        ws = self._workspace(self.workspace_bytes(audio.numel(), audio), audio.device, stream)
         fn = "vad_mfcc_ffn" if audio.dtype == torch.float32 else "vad_mfcc_ffn_i16"
         _lib.check(getattr(_lib.lib(), fn)(
             self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.numel(),
             self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
             _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), fn)
+        return out
+
+    def labels_unfused(self, audio, out=None, stream=None):
+        """The same labels through the two-kernel form (MFCC rows in HBM, then
+        the window kernel): the A/B baseline of the fused kernel."""
+        out = self._check_labels_call(audio, out)
+        if not isinstance(self.ffn, FFNClassifier):
+            raise ValueError("labels_unfused needs an FFN classifier")
+        need = self.n_frames(audio.numel()) * self.plan.mfcc_n * 4
+        ws = self._workspace(need, audio.device, stream)
+        _lib.check(_lib.lib().vad_mfcc_ffn_unfused(
+            self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.element_size(), audio.numel(),
+            self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
+            _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), "vad_mfcc_ffn_unfused")
         return out
 
     def process_clip(self, data):

@@ -31,6 +31,29 @@ def _require_cuda_tensor(t, name, dtype=torch.float32):
         raise ValueError(f"{name} must be contiguous")
 
 
+def check_out(out, shape, dtype, device, name="out"):
+    """A caller-supplied output must be exactly what the kernel writes: a
+    contiguous tensor of this shape and dtype on the input's device (anything
+    else would be an out-of-bounds or foreign-device write)."""
+    if not isinstance(out, torch.Tensor) or not out.is_cuda:
+        raise TypeError(f"{name} must be a CUDA (HIP) torch tensor")
+    if out.device != torch.device(device):
+        raise ValueError(f"{name} is on {out.device}, the input on {device}")
+    if out.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {out.dtype}")
+    if tuple(out.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(out.shape)}")
+    if not out.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return out
+
+
+def _out(out, shape, dtype, device, name="out"):
+    if out is None:
+        return torch.empty(shape, dtype=dtype, device=device)
+    return check_out(out, shape, dtype, device, name)
+
+
 def n_frames(n_samples, frame_size=400, hop=160):
     """Frames split_into_frames yields (file_processing.py:99: len - offset > size)."""
     return int(lib().vad_n_frames(int(n_samples), int(frame_size), int(hop)))
@@ -96,8 +119,7 @@ class MfccPlan:
     def spec(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
         """get_spec_mag (mfcc.py:59-61) of every frame -> (n, 256) fp32 (src fp32 or int16)."""
         frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
-        if out is None:
-            out = torch.empty((n, self.fft_n // 2), dtype=torch.float32, device=src.device)
+        out = _out(out, (n, self.fft_n // 2), torch.float32, src.device)
         fn = "vad_spec_i16" if src.dtype == torch.int16 else "vad_spec_f32"
         check(getattr(lib(), fn)(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
                                  stream_ptr(stream)), fn)
@@ -106,8 +128,7 @@ class MfccPlan:
     def mfcc(self, src, frame_len=None, frame_stride=None, n=None, out=None, stream=None):
         """get_mfcc (mfcc.py:67-69) of every frame -> (n, mfcc_n) fp32 (src fp32 or int16)."""
         frame_len, frame_stride, n = self._frames_args(src, frame_len, frame_stride, n)
-        if out is None:
-            out = torch.empty((n, self.mfcc_n), dtype=torch.float32, device=src.device)
+        out = _out(out, (n, self.mfcc_n), torch.float32, src.device)
         fn = "vad_mfcc_i16" if src.dtype == torch.int16 else "vad_mfcc_f32"
         check(getattr(lib(), fn)(self._h, ptr(src), frame_stride, frame_len, n, ptr(out),
                                  stream_ptr(stream)), fn)
@@ -128,8 +149,7 @@ class MfccPlan:
         if spec.dim() != 2 or spec.shape[1] != self.fft_n // 2:
             raise ValueError("spec must be (n, 256)")
         n = spec.shape[0]
-        if out is None:
-            out = torch.empty((n, self.mfcc_n), dtype=torch.float32, device=spec.device)
+        out = _out(out, (n, self.mfcc_n), torch.float32, spec.device)
         check(lib().vad_mfcc_from_spec_f32(self._h, ptr(spec), n, ptr(out), stream_ptr(stream)),
               "vad_mfcc_from_spec_f32")
         return out
@@ -179,8 +199,7 @@ class FfnPlan:
         if x.dim() != 2 or x.shape[1] != self.in_dim:
             raise ValueError(f"x must be (n, {self.in_dim})")
         n = x.shape[0]
-        if out is None:
-            out = torch.empty((n,), dtype=torch.uint8, device=x.device)
+        out = _out(out, (n,), torch.uint8, x.device)
         check(lib().vad_ffn_predict(self._h, ptr(x), n, ptr(out), stream_ptr(stream)),
               "vad_ffn_predict")
         return out
@@ -190,8 +209,7 @@ class FfnPlan:
         _require_cuda_tensor(mfcc, "mfcc")
         f, c = mfcc.shape
         rows = max(f - 5, 0)
-        if out is None:
-            out = torch.empty((rows,), dtype=torch.uint8, device=mfcc.device)
+        out = _out(out, (rows,), torch.uint8, mfcc.device)
         check(lib().vad_features_ffn(self._h, ptr(mfcc), f, c, int(mode), ptr(out),
                                      stream_ptr(stream)), "vad_features_ffn")
         return out
@@ -202,8 +220,7 @@ def window_features(mfcc, mode=_lib.FEAT_ANALYSER, out=None, stream=None):
     _require_cuda_tensor(mfcc, "mfcc")
     f, c = mfcc.shape
     rows = max(f - 5, 0)
-    if out is None:
-        out = torch.empty((rows, 3 * c), dtype=torch.float32, device=mfcc.device)
+    out = _out(out, (rows, 3 * c), torch.float32, mfcc.device)
     check(lib().vad_features_f32(ptr(mfcc), f, c, int(mode), ptr(out), stream_ptr(stream)),
           "vad_features_f32")
     return out

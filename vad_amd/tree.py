@@ -20,6 +20,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib, ptr, stream_ptr
+from .plan import _out
 
 _KEYS = ("feature", "threshold", "left", "right", "leaf", "nan_left", "classes")
 
@@ -117,12 +118,12 @@ class TreeClassifier:
         """Class indices (uint8, device) of device feature rows x (n, n_features) fp32."""
         if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32):
             raise TypeError("x must be a CUDA float32 tensor")
-        x = x.contiguous().reshape(-1, self.n_features)
+        x = x.contiguous().reshape(-1, self.n_features)  # kept alive until the launch is queued
         n = x.shape[0]
-        if out is None:
-            out = torch.empty((n,), dtype=torch.uint8, device=x.device)
+        out = _out(out, (n,), torch.uint8, x.device)
         check(lib().vad_tree_predict(self.plan.handle, ptr(x), n, ptr(out), stream_ptr(stream)),
               "vad_tree_predict")
+        _keep_for_stream(x, stream)
         return out
 
     def predict(self, X):
@@ -137,8 +138,17 @@ class TreeClassifier:
             raise TypeError("mfcc must be a CUDA float32 tensor")
         f, c = mfcc.shape
         rows = max(f - 5, 0)
-        if out is None:
-            out = torch.empty((rows,), dtype=torch.uint8, device=mfcc.device)
-        check(lib().vad_features_tree(self.plan.handle, ptr(mfcc.contiguous()), f, c, int(mode),
+        out = _out(out, (rows,), torch.uint8, mfcc.device)
+        m = mfcc.contiguous()  # a temporary copy must outlive the asynchronous kernel
+        check(lib().vad_features_tree(self.plan.handle, ptr(m), f, c, int(mode),
                                       ptr(out), stream_ptr(stream)), "vad_features_tree")
+        _keep_for_stream(m, stream)
         return out
+
+
+def _keep_for_stream(t, stream):
+    """A tensor read by a kernel queued on `stream` (not the current stream)
+    must not be recycled by the caching allocator for current-stream work
+    before that kernel ran."""
+    if stream is not None and stream != torch.cuda.current_stream(t.device):
+        t.record_stream(stream)
