@@ -105,6 +105,19 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims /* n_layers+1 */,
                         vad_ffn_plan** out);
 int vad_ffn_plan_destroy(vad_ffn_plan* plan);
 
+/* Arithmetic of the forward.  VAD_FFN_SPLIT_F16 (the default of the two
+ * specialised topologies 39-64-32-16-3 and 13-64-64-N): every GEMM operand
+ * split v = hi + lo into two f16 halves, lo*hi + hi*lo + hi*hi accumulated in
+ * f32 on v_mfma_f32_16x16x32_f16 (~22-bit operands, logits within a few f32
+ * ulps of an exact-f32 forward; tests/test_gpu_fullsize.py bounds it).
+ * VAD_FFN_EXACT_F32: v_mfma_f32_16x16x4_f32 (exact f32 products; every other
+ * topology always runs this).  set_arith returns VAD_EINVAL for split-f16 on
+ * a topology without it. */
+#define VAD_FFN_EXACT_F32 0
+#define VAD_FFN_SPLIT_F16 1
+int32_t vad_ffn_plan_arith(const vad_ffn_plan* plan);
+int vad_ffn_plan_set_arith(vad_ffn_plan* plan, int32_t arith);
+
 /* Feature rows (reference feature layout, 39 = 3 x 13):
  *   mode VAD_FEAT_ANALYSER: [Mn, M+1 - M-1, (M+2 - Mn) - (Mn - M-2)] with the
  *     centre MFCC normalised by the 5-frame mean / std (ddof 0)
@@ -125,6 +138,11 @@ int vad_features_f32(const float* mfcc, int64_t n_frames, int32_t mfcc_n, int32_
 int vad_features_ffn(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frames,
                      int32_t mfcc_n, int32_t mode, uint8_t* labels, void* stream);
 
+/* The same labels plus every window's fp32 logits, logits[i*n_classes + c]
+ * (before the softmax; parity tests of the FFN arithmetic). */
+int vad_features_ffn_logits(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frames,
+                            int32_t mfcc_n, int32_t mode, uint8_t* labels, float* logits, void* stream);
+
 /* FFN forward over caller-built feature rows x[i*in_dim + j] (predict on a
  * batch, ffn_trainer.py:106-116) -> labels[i]. */
 int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t* labels,
@@ -133,14 +151,20 @@ int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t*
 /* Clip path: framing + MFCC + features + FFN (dataset_creator/process_file
  * framing, file_processing.py:38-70, with the analyser's classifier call,
  * sklearn_analyser.py:71).  labels[i] for windows i < n_frames-5 of the clip.
- * One fused kernel (MFCC rows stay on chip, no workspace) for the reference
- * framing (frame 400, hop 160), the compiled 26-filter bank, a split-f16
- * FFN topology (39-64-32-16-3 or 13-64-64-N) and pair-aligned audio (8 B for
- * fp32, 4 B for int16: every torch allocation is); any other configuration
- * runs the MFCC and window kernels through `workspace` (device, >=
- * vad_mfcc_ffn_workspace_bytes(), which is 0 when the fused kernel applies). */
+ * Two forms, identical labels:
+ *   workspace != NULL (>= vad_mfcc_ffn_workspace_bytes(): the clip's MFCC
+ *     rows): the MFCC kernel, then the window kernel -- the faster form on
+ *     gfx950;
+ *   workspace == NULL: one fused kernel, the MFCC rows never leave the CU --
+ *     for the reference framing (frame 400, hop 160), the compiled 26-filter
+ *     bank, a split-f16 FFN topology (39-64-32-16-3 or 13-64-64-N) and
+ *     pair-aligned audio (8 B fp32 / 4 B int16: every torch allocation is);
+ *     VAD_EINVAL otherwise.  vad_mfcc_ffn_fusable() tells whether the plans
+ *     and framing qualify. */
 size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int64_t n_samples,
                                     int32_t frame_size, int32_t hop);
+int32_t vad_mfcc_ffn_fusable(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int32_t frame_size,
+                             int32_t hop);
 int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* audio,
                  int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                  uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
@@ -149,12 +173,6 @@ int vad_mfcc_ffn(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float
 int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const int16_t* audio,
                      int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode,
                      uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream);
-/* The two-kernel form (MFCC rows through the workspace, always required here)
- * of vad_mfcc_ffn (in_bytes 4) / vad_mfcc_ffn_i16 (in_bytes 2): the A/B
- * baseline of the fused kernel, identical labels. */
-int vad_mfcc_ffn_unfused(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int32_t in_bytes,
-                         int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
-                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Decision-tree plan: the classifier vad.py deploys

@@ -41,37 +41,38 @@ def test_fused_equals_two_kernel(torch_cuda, topo):
     a16 = a32.round().clamp(-32768, 32767).to(torch.int16)
     for mode in ("analyser", "offline"):
         pipe = _pipe(topo, mode)
-        assert pipe.workspace_bytes(a32.numel()) == 0  # the fused kernel applies
+        assert pipe.fusable
         for F in FRAMES:
             n = O.samples_for_frames(F)
             for a in (a32[:n], a16[:n]):
-                got = pipe.labels(a)
-                want = pipe.labels_unfused(a)
+                got = pipe.labels(a, fused=True)
+                want = pipe.labels(a)
                 assert got.numel() == F - 5
                 assert torch.equal(got, want), (topo, mode, F, a.dtype,
                                                 int((got != want).sum()))
 
 
-def test_fused_unaligned_and_fallbacks(torch_cuda):
-    """An audio view starting one sample in (not pair-aligned) and a 40-filter
-    plan run the two-kernel path through a workspace: same labels."""
+def test_fused_refuses_what_it_does_not_cover(torch_cuda):
+    """Unaligned audio (a view one sample in) and a 40-filter plan do not
+    qualify for the fused kernel: VadError without a workspace, and the
+    two-kernel form gives the labels of an aligned copy."""
     torch = torch_cuda
+    from vad_amd._lib import VadError
     from vad_amd.config import MfccConfig
     from vad_amd.ffn import FFNClassifier, random_layers
     from vad_amd.pipeline import VadPipeline
     F = 3000
-    clip = O.synth_clip(O.samples_for_frames(F) + 1, seed=22)
-    base = torch.from_numpy(clip).cuda()
+    base = torch.from_numpy(O.synth_clip(O.samples_for_frames(F) + 1, seed=22)).cuda()
     pipe = _pipe(TOPOS[0])
     view = base[1:]  # contiguous, 4-byte but not 8-byte aligned
     assert view.data_ptr() % 8 == 4
-    assert pipe.workspace_bytes(view.numel(), view) > 0
-    ref = pipe.labels_unfused(view.clone())
-    assert torch.equal(pipe.labels(view), ref)
-    p40 = VadPipeline(FFNClassifier(random_layers(TOPOS[0], seed=3)),
-                      cfg=MfccConfig(n_filters=40))
-    assert p40.workspace_bytes(base.numel()) > 0
-    assert torch.equal(p40.labels(base), p40.labels_unfused(base))
+    with pytest.raises(VadError):
+        pipe.labels(view, fused=True)
+    assert torch.equal(pipe.labels(view), pipe.labels(view.clone(), fused=True))
+    p40 = VadPipeline(FFNClassifier(random_layers(TOPOS[0], seed=3)), cfg=MfccConfig(n_filters=40))
+    assert not p40.fusable
+    with pytest.raises(VadError):
+        p40.labels(base, fused=True)
 
 
 def test_fused_out_checks(torch_cuda):
@@ -84,3 +85,4 @@ def test_fused_out_checks(torch_cuda):
         pipe.labels(a, out=torch.empty(495, dtype=torch.int32, device="cuda"))
     out = torch.empty(495, dtype=torch.uint8, device="cuda")
     assert pipe.labels(a, out=out) is out
+    assert pipe.labels(a, out=out, fused=True) is out

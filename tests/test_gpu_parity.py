@@ -3,8 +3,10 @@
 Tolerances:
   MFCC   per frame  ||d||_2 / ||ref||_2 <= 1e-4  and  max|d| <= 1e-4 * max|ref|
   spec   per frame  ||d||_2 / ||ref||_2 <= 1e-5 (float32 FFTs, different orders)
-  labels bit-exact wherever the fp64 oracle's top-2 logit margin exceeds
-         MARGIN_TOL; below it the count of disagreements is reported and bounded.
+  labels bit-exact on the fixture sets (their weights are calibrated so that
+         every window's fp64 top-2 logit margin exceeds 1e-3); on synthetic
+         clips with random weights, bit-exact wherever the margin exceeds
+         MARGIN_TOL.
 """
 import pickle
 
@@ -288,8 +290,10 @@ def test_analyser_features_and_labels_on_clip(torch_cuda, golden, fb26):
     marg = w["test_margin_ref39"]
     sure = marg > MARGIN_TOL
     np.testing.assert_array_equal(labels[sure], ref_l[sure])
-    bad = int((labels != ref_l).sum())
-    assert bad <= max(1, len(ref_l) // 100), bad
+    # every fixture window's margin exceeds 1e-3 (gen_golden calibrates the
+    # weights for it): the labels are exact, not just above MARGIN_TOL
+    assert marg.min() > 1e-3
+    np.testing.assert_array_equal(labels, ref_l)
     # same labels from the two-step device path
     m = pipe.mfcc(clip)
     np.testing.assert_array_equal(clf.plan.window_labels(m).cpu().numpy(), labels)
@@ -340,7 +344,8 @@ def test_analyser_trace_matches_reference(torch_cuda, golden, tmp_path):
     marg = O.ffn_margin(g["features"], layers_from(w, "ref39", 4))
     sure = np.concatenate([np.ones(5, bool), marg > MARGIN_TOL])
     np.testing.assert_array_equal(rets[sure], ref[sure])
-    assert int((rets != ref).sum()) <= 2
+    assert marg.min() > 1e-3  # calibrated fixture: every classified window is decisive
+    np.testing.assert_array_equal(rets, ref)
 
 
 def test_analyser_blocks_and_errors(torch_cuda, golden, tmp_path):

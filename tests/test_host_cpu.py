@@ -56,6 +56,27 @@ def test_abi_rejects_invalid_arguments():
     # fused clip entries without plans
     for fn in (lib.vad_mfcc_ffn, lib.vad_mfcc_ffn_i16):
         assert fn(None, None, None, 16000, 400, 160, 0, None, None, 0, None) == E
+    assert lib.vad_mfcc_ffn_fusable(None, None, 400, 160) == 0
+    assert lib.vad_mfcc_ffn_workspace_bytes(None, None, 16000, 400, 160) == 0
+
+
+def test_shipped_library_has_no_diagnostic_kernels():
+    """Diagnostic kernel instantiations (timestamps in place of MFCCs, an
+    L2-resident source, phase-1-only timing) exist only in libraries built
+    with -DVAD_DIAG_BUILD=n; the shipped library has none and reads no
+    environment variable that could select one."""
+    import re
+    import subprocess
+    from vad_amd import _lib
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"VAD_DIAG" not in data and b"VAD_FFN_EXACT" not in data
+    syms = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                          check=True).stdout + subprocess.run(["nm", _lib.LIB_PATH], capture_output=True,
+                                                              text=True).stdout
+    # mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>
+    diag = re.findall(r"mfcc_kernelI[fs]Li\d+ELi\d+ELb\dELi\d+ELi\d+ELi(\d+)ELi\d+E", syms)
+    assert diag, "mfcc_kernel instantiations not found in the symbol table"
+    assert set(diag) == {"0"}, sorted(set(diag))
 
 
 def test_stream_ring_size():

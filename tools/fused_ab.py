@@ -45,8 +45,8 @@ for name, topo in (("bl13", TOPOLOGY_BL13), ("ref39", TOPOLOGY_REF39)):
     for tag, a in (("f32", audio), ("i16", audio16)):
         out = torch.empty(F - 5, dtype=torch.uint8, device=dev)
         out2 = torch.empty_like(out)
-        fused = timeit(lambda: pipe.labels(a, out=out))
-        unfused = timeit(lambda: pipe.labels_unfused(a, out=out2))
+        fused = timeit(lambda: pipe.labels(a, out=out, fused=True))
+        unfused = timeit(lambda: pipe.labels(a, out=out2))
         same = bool(torch.equal(out, out2))
         res[f"{name}_{tag}"] = {"fused_ms": fused, "two_kernel_ms": unfused, "labels_equal": same}
 mf = torch.empty((F, 13), dtype=torch.float32, device=dev)

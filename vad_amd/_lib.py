@@ -21,6 +21,8 @@ VAD_EUNSUPPORTED = -2
 VAD_ENOMEM = -3
 FEAT_ANALYSER = 0
 FEAT_OFFLINE = 1
+FFN_EXACT_F32 = 0
+FFN_SPLIT_F16 = 1
 
 c_i32, c_i64, c_vp, c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t
 c_int = ctypes.c_int
@@ -40,8 +42,11 @@ SIGNATURES = {
     "vad_mfcc_from_spec_f32": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "vad_ffn_plan_create": (c_int, [c_i32, c_vp, c_vp, c_vp, c_vp]),
     "vad_ffn_plan_destroy": (c_int, [c_vp]),
+    "vad_ffn_plan_arith": (c_i32, [c_vp]),
+    "vad_ffn_plan_set_arith": (c_int, [c_vp, c_i32]),
     "vad_features_f32": (c_int, [c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "vad_features_ffn": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "vad_features_ffn_logits": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp]),
     "vad_ffn_predict": (c_int, [c_vp, c_vp, c_i64, c_vp, c_vp]),
     "vad_tree_plan_create": (c_int, [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp]),
     "vad_tree_plan_destroy": (c_int, [c_vp]),
@@ -57,8 +62,7 @@ SIGNATURES = {
                              c_vp]),
     "vad_mfcc_ffn_i16": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp, c_sz,
                                  c_vp]),
-    "vad_mfcc_ffn_unfused": (c_int, [c_vp, c_vp, c_vp, c_i32, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp,
-                                     c_sz, c_vp]),
+    "vad_mfcc_ffn_fusable": (c_i32, [c_vp, c_vp, c_i32, c_i32]),
     "vad_stream_ring_floats": (c_i64, [c_i64, c_i32]),
     "vad_stream_push_hop": (c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,

@@ -269,7 +269,7 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   // 32 s + k at layer 0, else 16 (2 s + (q >> 2)) + 4 (lane >> 4) + (q & 3):
   // the previous layer's accumulator rows as the lane holds them.
   std::vector<uint32_t> fragh;
-  const bool use_h3 = (ref39 || bl13) && !getenv("VAD_FFN_EXACT");
+  const bool use_h3 = ref39 || bl13;
   if (use_h3) {
     // every layer, output included: the block kernel runs bl13's output
     // layer on the VALU and reads only the hidden layers' slots (the first
@@ -320,6 +320,18 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   p->net = net;
   *out = p;
   return VAD_OK;
+}
+
+int32_t vad_ffn_plan_arith(const vad_ffn_plan* p) {
+  if (!p) return -1;
+  return p->net.fragh ? VAD_FFN_SPLIT_F16 : VAD_FFN_EXACT_F32;
+}
+
+int vad_ffn_plan_set_arith(vad_ffn_plan* p, int32_t arith) {
+  if (!p) return VAD_EINVAL;
+  if (arith == VAD_FFN_EXACT_F32) { p->net.fragh = nullptr; return VAD_OK; }
+  if (arith == VAD_FFN_SPLIT_F16 && p->fragh_dev) { p->net.fragh = p->fragh_dev; return VAD_OK; }
+  return VAD_EINVAL;
 }
 
 int vad_ffn_plan_destroy(vad_ffn_plan* p) {
@@ -473,6 +485,19 @@ int vad_features_ffn(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frame
   return (int)launch_ffn(ffn->net, 0, mfcc, rows, mfcc_n, mode, labels, (hipStream_t)stream);
 }
 
+int vad_features_ffn_logits(const vad_ffn_plan* ffn, const float* mfcc, int64_t n_frames, int32_t mfcc_n,
+                            int32_t mode, uint8_t* labels, float* logits, void* stream) {
+  if (!ffn || n_frames < 0 || mfcc_n <= 0 || mfcc_n > VAD_MAX_MFCC || (mode != 0 && mode != 1))
+    return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * mfcc_n) return VAD_EINVAL;
+  const int64_t rows = n_frames > 5 ? n_frames - 5 : 0;
+  if (rows == 0) return VAD_OK;
+  if (!mfcc || !labels || !logits) return VAD_EINVAL;
+  FfnDev net = ffn->net;
+  net.logits = logits;
+  return (int)launch_ffn(net, 0, mfcc, rows, mfcc_n, mode, labels, (hipStream_t)stream);
+}
+
 int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t* labels,
                     void* stream) {
   if (!ffn || n < 0) return VAD_EINVAL;
@@ -484,31 +509,35 @@ int vad_ffn_predict(const vad_ffn_plan* ffn, const float* x, int64_t n, uint8_t*
 size_t vad_mfcc_ffn_workspace_bytes(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int64_t n_samples,
                                     int32_t frame_size, int32_t hop) {
   if (!plan || !ffn) return 0;
-  // the fused kernel keeps the MFCC rows on chip (pair-aligned audio assumed:
-  // any torch allocation is)
-  if (mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, nullptr, 4)) return 0;
   const int64_t f = vad_n_frames(n_samples, frame_size, hop);
   return (size_t)f * plan->host.mfcc_n * sizeof(float);
 }
 
-// Shared body of vad_mfcc_ffn / vad_mfcc_ffn_i16: the fused kernel when the
-// configuration allows it, else MFCC rows through the workspace and the
-// window kernel.
+int32_t vad_mfcc_ffn_fusable(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, int32_t frame_size, int32_t hop) {
+  if (!plan || !ffn) return 0;
+  return mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, nullptr, 4) ? 1 : 0;
+}
+
+// Shared body of vad_mfcc_ffn / vad_mfcc_ffn_i16: with a workspace, the MFCC
+// kernel writes the rows there and the window kernel classifies them (the
+// faster form on gfx950); without one, the fused kernel keeps
+// them on chip.
 static int mfcc_ffn_entry(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int tin_bytes,
                           int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
-                          void* workspace, size_t workspace_bytes, void* stream, bool allow_fused = true) {
-  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1) ||
-      (tin_bytes != 2 && tin_bytes != 4))
+                          void* workspace, size_t workspace_bytes, void* stream) {
+  if (!plan || !ffn || n_samples < 0 || frame_size <= 0 || hop <= 0 || (mode != 0 && mode != 1))
     return VAD_EINVAL;
   const int64_t f = vad_n_frames(n_samples, frame_size, hop);
   if (f <= 5) return VAD_OK;
   if (!audio || !labels) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  if (allow_fused && mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, audio, tin_bytes))
+  if (!workspace) {
+    if (!mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, audio, tin_bytes)) return VAD_EINVAL;
     return (int)launch_mfcc_ffn(plan->dev, ffn->net, audio, tin_bytes, f, mode, labels, st);
+  }
   const size_t need = (size_t)f * plan->host.mfcc_n * sizeof(float);
-  if (!workspace || workspace_bytes < need) return VAD_EINVAL;
+  if (workspace_bytes < need) return VAD_EINVAL;
   float* mf = (float*)workspace;
   if (tin_bytes == 2)
     VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, (const int16_t*)audio, hop, frame_size, f, mf, st));
@@ -529,15 +558,6 @@ int vad_mfcc_ffn_i16(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const i
                      uint8_t* labels, void* workspace, size_t workspace_bytes, void* stream) {
   return mfcc_ffn_entry(plan, ffn, audio, 2, n_samples, frame_size, hop, mode, labels, workspace,
                         workspace_bytes, stream);
-}
-
-/* Two-kernel form of vad_mfcc_ffn (MFCC rows through the caller's workspace,
- * then the window kernel), kept for A/B measurement and tests. */
-int vad_mfcc_ffn_unfused(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const void* audio, int32_t in_bytes,
-                         int64_t n_samples, int32_t frame_size, int32_t hop, int32_t mode, uint8_t* labels,
-                         void* workspace, size_t workspace_bytes, void* stream) {
-  return mfcc_ffn_entry(plan, ffn, audio, in_bytes, n_samples, frame_size, hop, mode, labels, workspace,
-                        workspace_bytes, stream, false);
 }
 
 int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n) {

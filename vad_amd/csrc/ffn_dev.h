@@ -518,21 +518,17 @@ __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, 
   }
 }
 
-// Label of window lane & 15 (valid on every lane): layer-0 B operands
-// (lane (g, jw) holds features 32 s + 8 g + q of window jw) from X, the
-// split-f16 forward, the NaN flag, argmax.  MASK: X's columns IN .. 32 K0 - 1
-// hold stale data (not kept zero) and are zeroed in registers.
-template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, int IN, int XS, bool MASK,
-          class FH, class FB, class FV>
-__device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, const int* __restrict__ FL,
-                                                  int lane, FH fh, FB fb, FV fv, int n_classes) {
-  using TP = Topo<KS0, T1, T2, T3, T4, NC, NOVL>;
-  using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
+// Layer-0 B operands of window lane & 15 from X (lane (g, jw) holds
+// features 32 s + 8 g + q of window jw) and the window's NaN flag.  MASK:
+// X's columns IN .. 32 K0 - 1 hold stale data (not kept zero) and are zeroed
+// in registers.
+template <int K0, int IN, int XS, bool MASK>
+__device__ __forceinline__ int wave_tile_operands(const float* __restrict__ X, const int* __restrict__ FL,
+                                                  int lane, float (&x0)[K0][8]) {
   const int g = lane >> 4, jw = lane & 15;
-  float x0[HP::K0][8];
   const v4f* xr = reinterpret_cast<const v4f*>(X + jw * XS + 8 * g);
 #pragma unroll
-  for (int s = 0; s < HP::K0; ++s) {
+  for (int s = 0; s < K0; ++s) {
     const v4f lo4 = xr[8 * s], hi4 = xr[8 * s + 1];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -542,17 +538,41 @@ __device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, c
   }
   if constexpr (MASK) {
 #pragma unroll
-    for (int s = 0; s < HP::K0; ++s)
+    for (int s = 0; s < K0; ++s)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
         if (32 * s + q + 24 >= IN) x0[s][q] = 32 * s + 8 * g + q < IN ? x0[s][q] : 0.f;
   }
-  const int wnan = FL[jw];
-  f32x4 z;
+  return FL[jw];
+}
+
+// Label of window lane & 15 (valid on every lane) from its layer-0 operands:
+// the split-f16 forward, the NaN flag, argmax; z = its logits.
+template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, class FH, class FB, class FV>
+__device__ __forceinline__ int wave_tile_mlp(float (&x0)[(4 * KS0 + 31) / 32][8], int wnan, FH fh, FB fb, FV fv,
+                                             int n_classes, f32x4& z) {
   if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
   else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, FB, FV, NOVL>(fh, fb, fv, x0);
   if (wnan) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
   return argmax_classes(z, n_classes);
+}
+
+template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, int IN, int XS, bool MASK,
+          class FH, class FB, class FV>
+__device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, const int* __restrict__ FL,
+                                                  int lane, FH fh, FB fb, FV fv, int n_classes, f32x4& z) {
+  constexpr int K0 = (4 * KS0 + 31) / 32;
+  float x0[K0][8];
+  const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
+  return wave_tile_mlp<KS0, T1, T2, T3, T4, NC, NOVL>(x0, wnan, fh, fb, fv, n_classes, z);
+}
+
+// optional logits output (FfnDev::logits, tests): row w's fp32 logits
+__device__ __forceinline__ void store_logits(float* logits, int64_t w, const f32x4& z, int n_classes) {
+  if (!logits) return;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (c < n_classes) logits[w * n_classes + c] = z[c];
 }
 
 }  // namespace vad

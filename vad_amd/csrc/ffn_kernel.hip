@@ -63,7 +63,10 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
       x[s] = v;
     }
     const f32x4 z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
-    if (g == 0 && valid) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+    if (g == 0 && valid) {
+      labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+      store_logits(net.logits, w, z, net.n_classes);
+    }
   }
 }
 
@@ -259,7 +262,10 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
       }
       z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     }
-    if (g == 0 && wl < nwin) labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+    if (g == 0 && wl < nwin) {
+      labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
+      store_logits(net.logits, w, z, net.n_classes);
+    }
   }
 }
 
@@ -393,10 +399,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
       if (lane + 64 * q < kWRows) R[lane + 64 * q] = pre[q];
     load(tn < n_tiles ? tn : t, pre);
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
+    f32x4 z;
     const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false>(
-        X, FL, lane, fh, (const float*)fb, (const float*)fv, net.n_classes);
+        X, FL, lane, fh, (const float*)fb, (const float*)fv, net.n_classes, z);
     const int64_t w = t * kWTile + jw;
-    if (g == 0 && w < n_rows) labels[w] = (uint8_t)lab;
+    if (g == 0 && w < n_rows) {
+      labels[w] = (uint8_t)lab;
+      store_logits(net.logits, w, z, net.n_classes);
+    }
   };
   // VAD_FFN_PF tiles per trip, each with its own prefetch registers (no
   // copies at the back edge): a tile's rows are loaded PF tiles ahead

@@ -905,7 +905,7 @@ __device__ __forceinline__ Ptr launder(Ptr p) {
 
 #ifndef VAD_FUSED_DIAG
 #define VAD_FUSED_DIAG 0  // diagnostic builds only: 1 zero weight fragments (no loads), 2 no FFN,
-                          // 3 features only, 5 no FFN and the twiddles kept in VGPRs
+                          // 5 no FFN and the twiddles kept in VGPRs
 #endif
 
 constexpr int kRingRows = kTile + 4;
@@ -993,29 +993,27 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
   };
   // windows 16 wave .. 16 wave + 15 of ring buffer tt & 1 (row r = frame
   // fs + 64 tt - 4 + r; window 16 wave + jw starts at that row)
-  // windows of buffer tt & 1 after the DCT of tile td (td < 0: none); the
-  // split-f16 weight fragments of every layer are requested at once before
-  // the DCT (one L2 round trip, covered by the DCT and the features)
-  auto dct_ffn_tile = [&](int td, int tt) __attribute__((always_inline)) {
-    u4 frh[HP::NS][2];
+  // FFN of a 16-window tile of ring buffer tt & 1 (waves 0..3, windows
+  // 16 wave .. 16 wave + 15): features into the wave's FFT scratch slice,
+  // layer-0 operands, split-f16 forward, label.  The weight fragments are
+  // requested by the caller before the next tile's last sample batch, so the
+  // vmcnt wait for them does not also wait for those samples.
+  auto fetch_frags = [&](u4 (&frh)[HP::NS][2]) __attribute__((always_inline)) {
     if constexpr (VAD_FUSED_DIAG == 1) {
 #pragma unroll
       for (int sl = 0; sl < HP::NS; ++sl) frh[sl][0] = frh[sl][1] = (u4){0u, 0u, 0u, 0u};
     } else {
       load_fragh<HP>(reinterpret_cast<const uint32_t*>(launder(net.fragh)), lane, frh);
     }
-    if (td >= 0) dct_to_ring(td);
-    if constexpr (VAD_FUSED_DIAG == 2 || VAD_FUSED_DIAG == 5) return;
-    const LdsSlots fb{stbl + g4};
-    const LdsSlots fv{stbl + 4 * TP::NB + g4};
+  };
+  auto ffn_tile = [&](int tt, u4 (&frh)[HP::NS][2]) __attribute__((always_inline)) {
     const float* R = ring + (tt & 1) * kRingFloats + 16 * wave * MN;
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
-    if constexpr (VAD_FUSED_DIAG == 3) {
-      if (lane < 16) labels[fs + 16 * wave + lane] = (uint8_t)X[lane * XS + 3];
-      return;
-    }
-    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true>(
-        X, FL, lane, FragRegs{frh}, fb, fv, net.n_classes);
+    const LdsSlots fb{stbl + g4};
+    const LdsSlots fv{stbl + 4 * TP::NB + g4};
+    f32x4 z;
+    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true>(X, FL, lane, FragRegs{frh},
+                                                                                    fb, fv, net.n_classes, z);
     const int64_t i = fs + (int64_t)tt * kTile - 4 + 16 * wave + (lane & 15);
     if (lane < 16 && i >= wb && i < we) labels[i] = (uint8_t)lab;
   };
@@ -1053,7 +1051,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     VAD_MILESTONE(1);
     finish_b<false>(L, col, prow_a);
     __builtin_amdgcn_sched_barrier(0);
-    load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+    if (wave >= kDctGroups) load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);  // waves 0..3: below
     __builtin_amdgcn_sched_barrier(0);
     VAD_MILESTONE(0);
     store_a(u, gscr, j);
@@ -1061,19 +1059,35 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     finish_b<false>(L, col, prow_b);
     __builtin_amdgcn_sched_barrier(0);
     if (wave < kDctGroups) {
-      if (t >= 2) dct_ffn_tile(t - 1, t - 2);
-      else if (t == 1) dct_to_ring(0);
+      if (VAD_FUSED_DIAG != 2 && t >= 2) {
+        u4 frh[HP::NS][2];
+        fetch_frags(frh);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        dct_to_ring(t - 1);
+        ffn_tile(t - 2, frh);
+      } else {
+        load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+        if (t >= 1) dct_to_ring(t - 1);
+      }
     }
     lds_barrier();  // P complete; log-mel rows consumed; ring buffer (t-1) & 1 complete
     phase2a<SPEC>(plan, P, lm, wave, lane);
     lds_barrier();  // log-mel rows complete; P and the FFT scratch free
   }
-  if (wave < kDctGroups) {
-    if (n_t >= 2) dct_ffn_tile(n_t - 1, n_t - 2);
-    else dct_to_ring(n_t - 1);
+  if (VAD_FUSED_DIAG != 2 && wave < kDctGroups) {
+    u4 frh[HP::NS][2];
+    fetch_frags(frh);
+    dct_to_ring(n_t - 1);
+    if (n_t >= 2) ffn_tile(n_t - 2, frh);
   }
   lds_barrier();
-  if (wave < kDctGroups) dct_ffn_tile(-1, n_t - 1);
+  if (VAD_FUSED_DIAG != 2 && wave < kDctGroups) {
+    u4 frh[HP::NS][2];
+    fetch_frags(frh);
+    ffn_tile(n_t - 1, frh);
+  }
 }
 
 size_t mfcc_smem_bytes() { return kPBytes + kScrBytes + kLmBytes; }  // 157,696 B

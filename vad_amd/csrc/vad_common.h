@@ -49,6 +49,9 @@ struct FfnDev {
   // split-f16 MFMA weights (ref39 / bl13; null = exact f32 MFMA only):
   // [slot][64 lanes][4 words] of packed f16, slot = ((layer, mt, s), hi | lo)
   const uint32_t* fragh;
+  // optional (tests): the fp32 logits of every classified row,
+  // logits[row * n_classes + c] (null: labels only)
+  float* logits;
 };
 
 // Decision-tree node (tree_kernel.hip): internal if feature >= 0 (go left

@@ -4,7 +4,14 @@ duck-typed ``predict`` protocol the analyser uses
 
 Weights are Keras-layout ``W (in, out)``, ``b (out,)`` float32, stored as an
 ``.npz`` with keys ``W0, b0, W1, b1, ...`` (the reference never committed
-trained weights).  The forward pass runs on f32 MFMA.
+trained weights).
+
+Arithmetic: the two specialised topologies (39-64-32-16-3, 13-64-64-N) run
+"split-f16" by default -- every GEMM operand split v = hi + lo into f16
+halves, lo*hi + hi*lo + hi*hi accumulated in f32 on v_mfma_f32_16x16x32_f16
+(~22-bit operands: logits within a few f32 ulps of an exact-f32 forward);
+arith="f32" (and every other topology) runs exact f32 products on
+v_mfma_f32_16x16x4_f32.
 """
 from __future__ import annotations
 
@@ -49,8 +56,11 @@ def random_layers(dims=TOPOLOGY_REF39, seed=0):
 class FFNClassifier:
     """GPU FFN with the sklearn/Keras ``predict`` protocol."""
 
-    def __init__(self, layers):
+    def __init__(self, layers, arith="split_f16"):
         self.layers = [(np.asarray(w, np.float32), np.asarray(b, np.float32)) for w, b in layers]
+        if arith not in ("split_f16", "f32"):
+            raise ValueError("arith must be 'split_f16' or 'f32'")
+        self.arith_request = arith
         self._plan = None
 
     @classmethod
@@ -64,7 +74,14 @@ class FFNClassifier:
     def plan(self) -> FfnPlan:
         if self._plan is None:
             self._plan = FfnPlan(self.layers)
+            if self.arith_request == "f32":
+                self._plan.set_arith("f32")
         return self._plan
+
+    @property
+    def arith(self):
+        """The arithmetic the plan runs: "split_f16" or "f32"."""
+        return self.plan.arith
 
     @property
     def in_dim(self):
@@ -82,8 +99,9 @@ class FFNClassifier:
 
     # pickle support: weights travel, the device plan is rebuilt lazily
     def __getstate__(self):
-        return {"layers": self.layers}
+        return {"layers": self.layers, "arith": self.arith_request}
 
     def __setstate__(self, st):
         self.layers = st["layers"]
+        self.arith_request = st.get("arith", "split_f16")
         self._plan = None

@@ -5,8 +5,8 @@ process_file) -> split_into_frames (file_processing.py:80-103) -> per-frame
 get_mfcc -> 5-frame feature window (file_processing.py:40-70), with the
 analyser's classifier applied to every window (sklearn_analyser.py:52-71).
 Here a whole clip resident in HBM is framed, transformed and classified by
-one fused HIP kernel (the MFCC rows never leave the CU); the host only sizes
-buffers.
+two HIP kernels (MFCC rows through a workspace) or one fused kernel (MFCC rows
+kept on chip); the host only sizes buffers.
 """
 from __future__ import annotations
 
@@ -58,31 +58,36 @@ class VadPipeline:
         m = self.mfcc(audio, stream=stream)
         return window_features(m, self.mode if mode is None else mode, stream=stream)
 
-    def workspace_bytes(self, n_samples, audio=None):
-        """Device bytes vad_mfcc_ffn needs: 0 on the fused kernel (reference
-        framing, 26 filters, split-f16 FFN, pair-aligned audio), else the
-        (F, n_mfcc) fp32 MFCC rows of the two-kernel path."""
-        need = int(_lib.lib().vad_mfcc_ffn_workspace_bytes(
+    def workspace_bytes(self, n_samples):
+        """Device bytes of the two-kernel clip path: the (F, n_mfcc) fp32 MFCC rows."""
+        return int(_lib.lib().vad_mfcc_ffn_workspace_bytes(
             self.plan.handle, self.ffn.plan.handle, int(n_samples), self.cfg.frame_size, self.cfg.hop))
-        if need == 0 and audio is not None and audio.data_ptr() % (2 * audio.element_size()):
-            need = self.n_frames(n_samples) * self.plan.mfcc_n * 4  # unaligned: two kernels
-        return need
+
+    @property
+    def fusable(self):
+        """The fused kernel (no workspace) applies: reference framing, the
+        compiled 26-filter bank, a split-f16 FFN topology."""
+        return isinstance(self.ffn, FFNClassifier) and bool(_lib.lib().vad_mfcc_ffn_fusable(
+            self.plan.handle, self.ffn.plan.handle, self.cfg.frame_size, self.cfg.hop))
 
     def _workspace(self, need, device, stream):
         """Cached workspace per (device, stream): a buffer is never shared by
         work on two streams or handed to a kernel on another device."""
-        if need == 0:
-            return None
         s = stream if stream is not None else torch.cuda.current_stream(device)
         key = (device.index, s.cuda_stream)
         ws = self._ws.get(key)
         if ws is None or ws.numel() < need:
             with torch.cuda.stream(s):
-                ws = torch.empty((need,), dtype=torch.uint8, device=device)
+                ws = torch.empty((max(need, 1),), dtype=torch.uint8, device=device)
             self._ws[key] = ws
         return ws
 
-    def _check_labels_call(self, audio, out):
+    def labels(self, audio, out=None, stream=None, fused=False):
+        """uint8 (F-5,) labels of every window of a device clip; float32
+        samples, or int16 PCM as read from a wav file (identical labels).
+        fused=False: MFCC kernel + window kernel through a cached workspace
+        (the faster form); fused=True: the single fused kernel, MFCC rows kept
+        on chip (vad_mfcc_ffn with no workspace) -- identical labels."""
         if self.ffn is None:
             raise ValueError("pipeline has no FFN")
         if not (isinstance(audio, torch.Tensor) and audio.is_cuda
@@ -93,36 +98,17 @@ class VadPipeline:
             out = torch.empty((rows,), dtype=torch.uint8, device=audio.device)
         else:
             check_out(out, (rows,), torch.uint8, audio.device, "out")
-        return out
-
-    def labels(self, audio, out=None, stream=None):
-        """uint8 (F-5,) labels of every window of a device clip -- one fused
-        MFCC + features + FFN kernel (vad_mfcc_ffn); float32 samples, or int16
-        PCM as read from a wav file (identical labels)."""
-        out = self._check_labels_call(audio, out)
         if not isinstance(self.ffn, FFNClassifier):  # decision tree: MFCC, then windows
+            if fused:
+                raise ValueError("the fused kernel runs the FFN classifiers only")
             return self.ffn.window_labels(self.mfcc(audio, stream=stream), self.mode, out=out,
                                           stream=stream)
-        ws = self._workspace(self.workspace_bytes(audio.numel(), audio), audio.device, stream)
+        ws = None if fused else self._workspace(self.workspace_bytes(audio.numel()), audio.device, stream)
         fn = "vad_mfcc_ffn" if audio.dtype == torch.float32 else "vad_mfcc_ffn_i16"
         _lib.check(getattr(_lib.lib(), fn)(
             self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.numel(),
             self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
             _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), fn)
-        return out
-
-    def labels_unfused(self, audio, out=None, stream=None):
-        """The same labels through the two-kernel form (MFCC rows in HBM, then
-        the window kernel): the A/B baseline of the fused kernel."""
-        out = self._check_labels_call(audio, out)
-        if not isinstance(self.ffn, FFNClassifier):
-            raise ValueError("labels_unfused needs an FFN classifier")
-        need = self.n_frames(audio.numel()) * self.plan.mfcc_n * 4
-        ws = self._workspace(need, audio.device, stream)
-        _lib.check(_lib.lib().vad_mfcc_ffn_unfused(
-            self.plan.handle, self.ffn.plan.handle, _lib.ptr(audio), audio.element_size(), audio.numel(),
-            self.cfg.frame_size, self.cfg.hop, self.mode, _lib.ptr(out),
-            _lib.ptr(ws), 0 if ws is None else ws.numel(), _lib.stream_ptr(stream)), "vad_mfcc_ffn_unfused")
         return out
 
     def process_clip(self, data):

@@ -187,6 +187,16 @@ class FfnPlan:
     def n_classes(self):
         return self.dims[-1]
 
+    @property
+    def arith(self):
+        """"split_f16" (v_mfma_f32_16x16x32_f16 on hi/lo f16 halves of every
+        operand, the specialised topologies' default) or "f32" (exact f32 MFMA)."""
+        return "split_f16" if lib().vad_ffn_plan_arith(self._h) == _lib.FFN_SPLIT_F16 else "f32"
+
+    def set_arith(self, arith):
+        code = {"split_f16": _lib.FFN_SPLIT_F16, "f32": _lib.FFN_EXACT_F32}[arith]
+        check(lib().vad_ffn_plan_set_arith(self._h, code), "vad_ffn_plan_set_arith")
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value and _lib._lib is not None:
@@ -213,6 +223,19 @@ class FfnPlan:
         check(lib().vad_features_ffn(self._h, ptr(mfcc), f, c, int(mode), ptr(out),
                                      stream_ptr(stream)), "vad_features_ffn")
         return out
+
+
+def window_logits(ffn_plan, mfcc, mode=_lib.FEAT_ANALYSER, stream=None):
+    """(labels uint8 (F-5,), logits fp32 (F-5, n_classes)) of every window of
+    an MFCC sequence, from the same kernel as FfnPlan.window_labels."""
+    _require_cuda_tensor(mfcc, "mfcc")
+    f, c = mfcc.shape
+    rows = max(f - 5, 0)
+    labels = torch.empty((rows,), dtype=torch.uint8, device=mfcc.device)
+    logits = torch.empty((rows, ffn_plan.n_classes), dtype=torch.float32, device=mfcc.device)
+    check(lib().vad_features_ffn_logits(ffn_plan.handle, ptr(mfcc), f, c, int(mode), ptr(labels), ptr(logits),
+                                        stream_ptr(stream)), "vad_features_ffn_logits")
+    return labels, logits
 
 
 def window_features(mfcc, mode=_lib.FEAT_ANALYSER, out=None, stream=None):
