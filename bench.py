@@ -104,6 +104,68 @@ def _cpu_chunks(args):
     return n
 
 
+def _cpu_per_frame(args):
+    """Reference-shaped loop (variant (i) of SURVEY 8(d)): per frame
+    mfcc.get_mfcc (np.fft.fft -> dot -> log10 -> dct -> lifter, mfcc.py:67-78)
+    into a 5-frame buffer, per window the analyser's (1, 39) feature row and
+    a batch-1 FFN predict (sklearn_analyser.py:52-71) -- the oracle's
+    per-frame functions, one core.  Returns frames done in `seconds`."""
+    seconds, dims = args
+    from threadpoolctl import threadpool_limits
+    from oracle import vad_oracle as O
+    from vad_amd.ffn import random_layers
+    layers = random_layers(dims, seed=3)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    clip = O.synth_clip(160 * 20000 + 241, seed=1)
+    fr = O.frame_matrix(clip)
+    with threadpool_limits(limits=1):
+        buf, n, t0 = [], 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            buf.append(O.get_mfcc(fr[n % len(fr)], 512, fb, 13))
+            if len(buf) > 5:
+                buf.pop(0)
+            if len(buf) == 5:
+                x = O.window_features(np.stack(buf))[None, :dims[0]]
+                O.ffn_labels(x, layers)
+            n += 1
+    return n
+
+
+def host_facts():
+    """CPU model, cores this process may use, NumPy / SciPy versions."""
+    import scipy
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "cores_available": len(os.sched_getaffinity(0)),
+            "numpy": np.__version__, "scipy": scipy.__version__}
+
+
+def cpu_baseline_per_frame(dims, seconds=5.0):
+    """Variant (i): the reference-shaped per-frame loop on 1 core and on up to
+    16 cores (one spawned process each, like dataset_creator.py:84's Pool)."""
+    import multiprocessing as mp
+    n1 = _cpu_per_frame((seconds, tuple(dims)))
+    one = {"value": n1 / seconds, "unit": "frames/s", "cores": 1, "kind": "port",
+           "sample": f"{n1} frames, per-frame get_mfcc + per-window features + batch-1 FFN, {seconds:.0f} s"}
+    n_proc = max(1, min(16, len(os.sched_getaffinity(0))))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(n_proc) as pool:
+        pool.map(_cpu_per_frame, [(0.5, tuple(dims))] * n_proc)  # imports, warm caches
+        t0 = time.perf_counter()
+        n = sum(pool.map(_cpu_per_frame, [(seconds, tuple(dims))] * n_proc))
+        el = time.perf_counter() - t0
+    allc = {"value": n / el, "unit": "frames/s", "cores": n_proc, "kind": "port",
+            "sample": f"{n} frames on {n_proc} processes x 1 thread, same per-frame loop, {el:.1f} s"}
+    return one, allc
+
+
 def cpu_baseline_all(dims, frames_per_chunk=20000, seconds=6.0):
     """The same oracle loop on every host core this process may use (at most
     16, the GPU box's CPU share), one process per core (spawned: no fork of
@@ -121,6 +183,38 @@ def cpu_baseline_all(dims, frames_per_chunk=20000, seconds=6.0):
                       f"{el:.1f} s"}
 
 
+def feed_frame_latency(dev, calls=2000, warm=50):
+    """Per-call latency of the drop-in SKLearnAnalyzer.feed_frame (the API
+    vad.py:52 calls once per 25 ms block): one 400-sample frame in, the
+    frame three calls back or None out -- H2D copy, the MFCC + features + FFN
+    kernels on the stream's device state, the label read back.  A 2-class
+    39-64-32-16-2 network (labels 0/1 only, as vad.py's dispatch expects)."""
+    import tempfile
+    from oracle import vad_oracle as O
+    from vad_amd.ffn import random_layers, save_layers
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "ffn.npz")
+        save_layers(path, random_layers((39, 64, 32, 16, 2), seed=3))
+        an = SKLearnAnalyzer(path)
+    clip = O.synth_clip(400 * (calls + warm + 5), seed=2).reshape(-1, 400)
+    an.load_init_inactive_frames(list(clip[:5]))
+    frames = list(clip[5:])
+    for f in frames[:warm]:
+        an.feed_frame(f)
+    per = []
+    for f in frames[warm:warm + calls]:
+        t0 = time.perf_counter()
+        an.feed_frame(f)
+        per.append(time.perf_counter() - t0)
+    per = np.sort(np.asarray(per)) * 1e3
+    return {"ms_per_call_mean": float(per.mean()), "p50": float(per[len(per) // 2]),
+            "p99": float(per[int(0.99 * len(per))]), "calls": calls,
+            "reference_ms_per_call": 3.07,
+            "reference_source": "SURVEY.md section 6: SKLearnAnalyzer.feed_frame on this container's CPU "
+                                "(not re-measured here: the reference cannot travel to the GPU box)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,6 +223,9 @@ def main():
     ap.add_argument("--frames", type=int, default=1_000_000)
     ap.add_argument("--ffn", default="bl13", choices=["bl13", "ref39"])
     ap.add_argument("--no-cpu", action="store_true")
+    # a GPU that was idle starts at low clocks and ramps for ~30 ms of load:
+    # warm-up steps continue (untimed) until this much warm-up time has passed
+    ap.add_argument("--min-warmup-s", type=float, default=0.5)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,14 +255,29 @@ def main():
     gather = LabelGather(F - 5, dev) if world > 1 else None
 
     def step():
-        pipe.mfcc(audio, out=mfcc)                       # HIP MFCC kernel
-        ffn_plan.window_labels(mfcc, out=labels)          # HIP features + MFMA FFN kernel
+        # vad_mfcc_ffn with a workspace: the MFCC kernel, then the window
+        # features + split-f16 MFMA FFN kernel (the faster of the two clip
+        # forms on gfx950; the fused single kernel is timed below)
+        pipe.labels(audio, out=labels)
         if world > 1:
             gather(labels)                                 # RCCL: decisions -> rank 0
 
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    extra = 0
+    while time.perf_counter() - t_w < args.min_warmup_s:
+        for _ in range(10):
+            step()
+        extra += 10
+        torch.cuda.synchronize()
+    if world > 1:  # every rank warms up equally long
+        t = torch.tensor([extra], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        for _ in range(int(t.item()) - extra):
+            step()
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -200,6 +312,12 @@ def main():
         return ev[0].elapsed_time(ev[nb]) / (nb * batch), pct
     mfcc_ms, mfcc_pct = kernel_ms(lambda: pipe.mfcc(audio, out=mfcc))
     ffn_ms, ffn_pct = kernel_ms(lambda: ffn_plan.window_labels(mfcc, out=labels))
+    # the fused single-kernel clip form (MFCC rows kept on chip) and the FFN
+    # on exact-f32 MFMA, beside the headline's forms
+    fused_ms, fused_pct = kernel_ms(lambda: pipe.labels(audio, out=labels, fused=True))
+    exact = FFNClassifier(layers, arith="f32")
+    ffn_f32_ms, _ = kernel_ms(lambda: exact.plan.window_labels(mfcc, out=labels))
+    del exact
     # the same clip as int16 PCM (what vad.py reads; exact: the samples are
     # integers in the int16 range), MFCC kernel only -- reported beside `value`
     audio16 = audio.to(torch.int16)
@@ -226,11 +344,17 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_steps": extra,
             "ms_per_step": el * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
+            "dtype_detail": "MFCC: fp32 (packed-fp32 VALU FFT, fp32 mel / log10 / DCT); FFN: split-f16x3 "
+                            "MFMA (v_mfma_f32_16x16x32_f16 on hi/lo f16 halves of every operand, "
+                            "lo*hi + hi*lo + hi*hi, f32 accumulate; logit error within 1.5x of an "
+                            "exact-f32 forward, tests/test_gpu_fullsize.py); exact-f32 FFN timed in "
+                            "kernels_ms.ffn_kernel_exact_f32",
             "data": "synthetic (int16-range noise, 10**U(0,4) segment gains, 5% digital silence; "
                     "seeded random-init FFN weights)",
             "config": {"workload": "C3/C4: MFCC + FFN VAD forward, 1 clip of F frames per GPU "
@@ -250,16 +374,24 @@ def main():
                         "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": MFCC_FLOPS_PER_FRAME * F / (mfcc_ms * 1e-3) / 1e12 / VALU_PEAK_TFS,
                         "flops_per_frame": MFCC_FLOPS_PER_FRAME},
-            "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms},
-            "kernels_ms_pct": {"mfcc_kernel": mfcc_pct, "ffn_kernel": ffn_pct},
+            "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms,
+                           "ffn_kernel_exact_f32": ffn_f32_ms, "mfcc_ffn_fused_kernel": fused_ms},
+            "kernels_ms_pct": {"mfcc_kernel": mfcc_pct, "ffn_kernel": ffn_pct,
+                               "mfcc_ffn_fused_kernel": fused_pct},
             "mfcc_int16_input": {"avg_launch_ms": mfcc16_ms,
                                  "frames_per_s": F / (mfcc16_ms * 1e-3),
                                  "algorithmic_bytes_per_frame": 160 * 2 + 13 * 4,
                                  "achieved_GBps": (160 * 2 + 13 * 4) * F / (mfcc16_ms * 1e-3) / 1e9},
         }
+        if world == 1:
+            out["feed_frame_latency"] = feed_frame_latency(dev)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(layers)
             out["cpu_baseline_all_cores"] = cpu_baseline_all(tuple(topo))
+            pf1, pfall = cpu_baseline_per_frame(tuple(topo))
+            out["cpu_baseline_per_frame"] = pf1
+            out["cpu_baseline_per_frame_all_cores"] = pfall
+            out["cpu_host"] = host_facts()
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
