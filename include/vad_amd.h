@@ -36,6 +36,7 @@ extern "C" {
 #define VAD_EINVAL (-1)        /* bad argument (null, negative size, ...) */
 #define VAD_EUNSUPPORTED (-2)  /* valid for the reference, not built here (fft_n != 512, ...) */
 #define VAD_ENOMEM (-3)
+#define VAD_ERCCL (-4)         /* RCCL returned an error: vad_rccl_error_string() */
 
 typedef struct vad_mfcc_plan vad_mfcc_plan;
 typedef struct vad_ffn_plan vad_ffn_plan;
@@ -261,6 +262,30 @@ int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, 
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU clip sharding: one process per GPU, each
+ * classifying its shard (vad_amd/dist.py split_clip: windows [w_lo, w_hi)
+ * from samples [160 w_lo, 160 (w_hi + 4) + 401)), then ONE collective: the
+ * gather of the per-window uint8 decisions to the root over RCCL / xGMI.
+ * The reference's only parallelism is dataset_creator.py:84's process pool;
+ * these entries replace nothing there -- they are the host-agnostic form of
+ * vad_amd.dist.LabelGather (torch.distributed "nccl").  RCCL is resolved at
+ * run time (the process's loaded copy, else librccl.so.1).
+ * ------------------------------------------------------------------------- */
+#define VAD_RCCL_ID_BYTES 128
+typedef struct vad_rccl_comm vad_rccl_comm;
+int vad_rccl_available(void);
+const char* vad_rccl_error_string(void);
+/* ncclGetUniqueId on the root; the caller ships the 128 bytes to every rank. */
+int vad_rccl_unique_id(void* id_out /* VAD_RCCL_ID_BYTES */);
+/* ncclCommInitRank on the current HIP device. */
+int vad_rccl_init(vad_rccl_comm** out, int32_t nranks, const void* id, int32_t rank);
+/* ncclGather of `count` uint8 per rank: recv (root only) = nranks * count,
+ * rank r's block at recv + r * count.  Enqueued on `stream`. */
+int vad_rccl_gather_u8(vad_rccl_comm* comm, const uint8_t* send, uint8_t* recv, size_t count, int32_t root,
+                       void* stream);
+int vad_rccl_destroy(vad_rccl_comm* comm);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,7 @@ RCCL through the same code with backend "nccl")."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -55,3 +56,59 @@ def test_gather_labels_gloo(world):
     assert got == [(i * 3) % 7 for i in range(11)]
     for step, f in enumerate(fixed):
         assert f == [[r * 10 + step] * 4 for r in range(world)]
+
+
+def test_split_clip_covers_every_window_once():
+    from oracle import vad_oracle as O
+    from vad_amd.dist import split_clip
+    for F in (6, 7, 100, 1001, 1_000_000):
+        L = O.samples_for_frames(F)
+        for world in (1, 2, 3, 8):
+            shards = [split_clip(L, r, world) for r in range(world)]
+            assert shards[0].win_lo == 0 and shards[-1].win_hi == F - 5
+            for a, b in zip(shards, shards[1:]):
+                assert a.win_hi == b.win_lo
+            for s in shards:
+                if s.n_windows:
+                    # the segment's own framing yields exactly its windows + 5 frames
+                    assert O.n_frames(s.sample_hi - s.sample_lo) == s.n_windows + 5
+                    assert s.sample_lo == 160 * s.win_lo and s.sample_hi <= L
+
+
+def _oracle_shard_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import vad_oracle as O
+    from vad_amd.dist import gather_clip_labels, split_clip
+    from vad_amd.ffn import TOPOLOGY_BL13, random_layers
+    layers = random_layers(TOPOLOGY_BL13, seed=3)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    clip = O.synth_clip(O.samples_for_frames(3001), seed=12)
+    sh = split_clip(len(clip), rank, world)
+
+    def labels(x):
+        return O.ffn_labels(O.analyser_features_fast(O.mfcc_batch(x, fb))[:, :13], layers)
+    lab = torch.from_numpy(labels(clip[sh.sample_lo:sh.sample_hi]).astype(np.uint8))
+    full = gather_clip_labels(lab, sh)
+    if rank == 0:
+        q.put(bool(np.array_equal(full.numpy(), labels(clip).astype(np.uint8))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_clip_labels_equal_whole_clip(world):
+    """The halo rule on the CPU oracle: every rank classifies its segment,
+    the gathered labels are the whole clip's (windows at every cut included)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oracle_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    same = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert same

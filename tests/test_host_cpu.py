@@ -57,6 +57,10 @@ def test_abi_rejects_invalid_arguments():
     for fn in (lib.vad_mfcc_ffn, lib.vad_mfcc_ffn_i16):
         assert fn(None, None, None, 16000, 400, 160, 0, None, None, 0, None) == E
     assert lib.vad_mfcc_ffn_fusable(None, None, 400, 160) == 0
+    # RCCL entries: argument checks before RCCL is touched
+    assert lib.vad_rccl_init(None, 1, None, 0) == E
+    assert lib.vad_rccl_gather_u8(None, None, None, 16, 0, None) == E
+    assert lib.vad_rccl_destroy(None) == _lib.VAD_OK
     assert lib.vad_mfcc_ffn_workspace_bytes(None, None, 16000, 400, 160) == 0
 
 

@@ -19,6 +19,7 @@ VAD_OK = 0
 VAD_EINVAL = -1
 VAD_EUNSUPPORTED = -2
 VAD_ENOMEM = -3
+VAD_ERCCL = -4
 FEAT_ANALYSER = 0
 FEAT_OFFLINE = 1
 FFN_EXACT_F32 = 0
@@ -67,6 +68,12 @@ SIGNATURES = {
     "vad_stream_push_hop": (c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                 c_vp]),
+    "vad_rccl_available": (c_int, []),
+    "vad_rccl_error_string": (ctypes.c_char_p, []),
+    "vad_rccl_unique_id": (c_int, [c_vp]),
+    "vad_rccl_init": (c_int, [c_vp, c_i32, c_vp, c_i32]),
+    "vad_rccl_gather_u8": (c_int, [c_vp, c_vp, c_vp, c_sz, c_i32, c_vp]),
+    "vad_rccl_destroy": (c_int, [c_vp]),
 }
 
 
@@ -98,6 +105,8 @@ def check(code, what):
     if code != VAD_OK:
         names = {VAD_EINVAL: "invalid argument", VAD_EUNSUPPORTED: "unsupported configuration",
                  VAD_ENOMEM: "out of memory"}
+        if code == VAD_ERCCL:
+            raise VadError(f"{what} failed: RCCL: {lib().vad_rccl_error_string().decode()}")
         raise VadError(f"{what} failed: {names.get(code, f'hipError_t {code}')}")
 
 

@@ -17,7 +17,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvad_amd.so")
 ARCH = os.environ.get("VAD_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["capi.hip", "mfcc_kernel.hip", "ffn_kernel.hip", "tree_kernel.hip",
-           "dataset_kernel.hip", "csv_format.hip", "simple_kernel.hip", "stream_kernel.hip"]
+           "dataset_kernel.hip", "csv_format.hip", "simple_kernel.hip", "stream_kernel.hip", "rccl.hip"]
 # per-translation-unit code-generation flags: the FFT's packed-fp32 chains
 # run ~5% faster under the ILP-oriented machine scheduler (fewer dependent
 # pairs back to back, i.e. fewer hazard s_nops and stalls)
@@ -30,6 +30,7 @@ UNIT_FLAGS = {
     "simple_kernel.hip": [],
     "stream_kernel.hip": [],
     "capi.hip": [],
+    "rccl.hip": [],
 }
 
 
@@ -66,7 +67,7 @@ def build(force=False, verbose=True, defines=(), out=None):
         objs.append(obj)
     if any(p.wait() != 0 for p in procs):
         raise subprocess.CalledProcessError(1, "hipcc -c")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp"] + objs + ["-ldl"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
