@@ -67,6 +67,21 @@ int vad_mfcc_plan_destroy(vad_mfcc_plan* plan);
 int32_t vad_mfcc_plan_variant(const vad_mfcc_plan* plan);
 int vad_mfcc_plan_set_variant(vad_mfcc_plan* plan, int32_t variant);
 
+/* Optional stages NOT in the reference (mfcc.py:59-61 feeds the raw frame to
+ * the FFT: rectangular window, no pre-emphasis; BASELINE's north_star names
+ * both).  Default off; with both off every output is bit-identical to a plan
+ * that never had them.  Parity for them is pinned to the oracle's
+ * restatement only (python_speech_features conventions).
+ *   set_window: multiply sample t of every frame by window_host[t] (t < len
+ *     <= 512, e.g. numpy.hamming(400)) before the FFT; NULL removes it.
+ *     Windowed plans run the runtime-table kernel (variant kSpecWindow = 3).
+ *   vad_preemphasis_f32: y[r][0] = x[r][0], y[r][t] = x[r][t] - coeff
+ *     x[r][t-1] for each of n_rows rows of row_len samples (a clip: one row),
+ *     out of place -- run before framing. */
+int vad_mfcc_plan_set_window(vad_mfcc_plan* plan, const float* window_host, int32_t len);
+int vad_preemphasis_f32(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t row_stride,
+                        float coeff, void* stream);
+
 /* Frames f = 0..n_frames-1 start at src + f*frame_stride and hold frame_len
  * samples (fp32); only the first min(frame_len, 512) feed the 512-point FFT
  * (np.fft.fft(x, 512) zero-pads / truncates, mfcc.py:61).

@@ -154,3 +154,22 @@ def test_tree_table_roundtrip(tmp_path, golden):
     for k in ("feature", "threshold", "left", "right", "leaf", "nan_left", "classes_"):
         assert np.array_equal(getattr(t, k), getattr(u, k))
     assert u.n_features == t.n_features == 39
+
+
+def test_optional_stages_default_off_and_oracle_restatement():
+    """Pre-emphasis / window are off by default (the reference has neither);
+    the oracle's restatement reduces to the reference path when they are
+    neutral."""
+    from oracle import vad_oracle as O
+    from vad_amd.config import MfccConfig
+    cfg = MfccConfig()
+    assert cfg.preemph is None and cfg.window is None
+    clip = O.synth_clip(O.samples_for_frames(300), seed=64)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    base = O.mfcc_batch(clip, fb)
+    np.testing.assert_array_equal(O.mfcc_batch(clip, fb, window=np.ones(400)), base)
+    np.testing.assert_array_equal(O.mfcc_batch(clip, fb, preemph=0.0), base)
+    y = O.preemphasis(clip, 0.97)
+    assert y[0] == clip[0]
+    np.testing.assert_allclose(y[1:], clip[1:] - np.float32(0.97) * clip[:-1], rtol=0, atol=0)
+    assert not np.allclose(O.mfcc_batch(clip, fb, window=np.hamming(400)), base)

@@ -36,6 +36,8 @@ SIGNATURES = {
     "vad_mfcc_plan_destroy": (c_int, [c_vp]),
     "vad_mfcc_plan_variant": (c_i32, [c_vp]),
     "vad_mfcc_plan_set_variant": (c_int, [c_vp, c_i32]),
+    "vad_mfcc_plan_set_window": (c_int, [c_vp, c_vp, c_i32]),
+    "vad_preemphasis_f32": (c_int, [c_vp, c_vp, c_i64, c_i64, c_i64, ctypes.c_float, c_vp]),
     "vad_spec_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
     "vad_mfcc_f32": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),
     "vad_spec_i16": (c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp]),

@@ -24,9 +24,15 @@ PROCESSING_FRAME_INDEX = 2   # sklearn_analyser.py:19
 
 @dataclass(frozen=True)
 class MfccConfig:
-    """One MFCC configuration.  Pre-emphasis and a Hamming window are NOT part
-    of the reference pipeline (mfcc.py:59-61 feeds raw frames to the FFT), so
-    there is no switch for them: adding either would break parity."""
+    """One MFCC configuration.
+
+    preemph / window are optional stages BASELINE's north_star names that the
+    reference pipeline does NOT have (mfcc.py:59-61 feeds raw frames to the
+    FFT): default off, and with both off every output is bit-identical to the
+    reference-parity path.  preemph = a runs y[t] = x[t] - a x[t-1] over the
+    clip before framing; window = "hamming" multiplies each frame by
+    numpy.hamming(frame_size) before the FFT (python_speech_features
+    conventions; parity pinned to the oracle's restatement only)."""
 
     sample_rate: int = SAMPLERATE
     frame_size: int = FRAME_SIZE
@@ -37,3 +43,5 @@ class MfccConfig:
     low_hz: float = LOW_HZ
     high_hz: float = HIGH_HZ
     lifter: int = 22   # mfcc.py:85 default, used by every reference call
+    preemph: float | None = None   # off: not in the reference
+    window: str | None = None      # None (rectangular, the reference) or "hamming"

@@ -16,7 +16,9 @@ using namespace vad;
 struct vad_mfcc_plan {
   MfccDev host;      // host copy (for introspection)
   MfccDev* dev;      // device copy read by the kernels
-  int spec;          // 1/2: equals the compile-time Mel26/Mel40 tables bit for bit
+  int spec;          // 1/2: equals the compile-time Mel26/Mel40 tables bit for bit;
+                     // kSpecWindow: an analysis window is set
+  int table_spec;    // the compile-time table match without a window
 };
 
 // Does the runtime plan equal compile-time table T (taps, ranges, DCT rows)?
@@ -123,7 +125,7 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     const double a = -2.0 * M_PI * k / 512.0;
     h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
   }
-  p->spec = matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
+  p->spec = p->table_spec = matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
   hipError_t e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
   if (e != hipSuccess) { free(p); return (int)e; }
   e = hipMemcpy(p->dev, &h, sizeof(MfccDev), hipMemcpyHostToDevice);
@@ -141,8 +143,27 @@ int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
 
 int32_t vad_mfcc_plan_variant(const vad_mfcc_plan* p) { return p ? p->spec : -1; }
 
+int vad_mfcc_plan_set_window(vad_mfcc_plan* p, const float* window_host, int32_t len) {
+  if (!p) return VAD_EINVAL;
+  if (window_host && (len <= 0 || len > kFftN)) return VAD_EINVAL;
+  for (int t = 0; t < kFftN; ++t) p->host.window[t] = window_host && t < len ? window_host[t] : 0.f;
+  const hipError_t e = hipMemcpy(p->dev->window, p->host.window, sizeof(p->host.window), hipMemcpyHostToDevice);
+  if (e != hipSuccess) return (int)e;
+  p->spec = window_host ? kSpecWindow : p->table_spec;
+  return VAD_OK;
+}
+
+int vad_preemphasis_f32(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t row_stride,
+                        float coeff, void* stream) {
+  if (n_rows < 0 || row_len < 0 || row_stride < row_len) return VAD_EINVAL;
+  if (n_rows == 0 || row_len == 0) return VAD_OK;
+  if (!x || !y || x == y) return VAD_EINVAL;
+  return (int)launch_preemphasis(x, y, n_rows, row_len, row_stride, coeff, (hipStream_t)stream);
+}
+
 int vad_mfcc_plan_set_variant(vad_mfcc_plan* p, int32_t variant) {
   if (!p) return VAD_EINVAL;
+  if (p->spec == kSpecWindow) return VAD_EINVAL;  // windowed plans run the runtime-table kernel
   if (variant == 0) { p->spec = 0; return VAD_OK; }
   if (variant == 1 && matches_table<Mel26>(p->host)) { p->spec = 1; return VAD_OK; }
   if (variant == 2 && matches_table<Mel40>(p->host)) { p->spec = 2; return VAD_OK; }
@@ -161,7 +182,7 @@ int vad_spec_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
                  float* spec, void* stream) {
   int r = check_frames(p, src, stride, len, n, spec);
   if (r || n == 0) return r;
-  return (int)launch_mfcc(1, p->dev, 0, src, stride, len, n, spec, (hipStream_t)stream);
+  return (int)launch_mfcc(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
 }
 
 int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32_t len, int64_t n,
@@ -175,7 +196,7 @@ int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
                  float* spec, void* stream) {
   int r = check_frames(p, src, stride, len, n, spec);
   if (r || n == 0) return r;
-  return (int)launch_mfcc_i16(1, p->dev, 0, src, stride, len, n, spec, (hipStream_t)stream);
+  return (int)launch_mfcc_i16(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
 }
 
 int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,

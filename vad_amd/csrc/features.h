@@ -9,9 +9,17 @@ namespace vad {
 // centre-2 .. centre+2): (Mn, M+1 - M-1, (M+2 - Mn) - (Mn - M-2)) with Mn the
 // centre normalised by the window mean / std (ddof 0) in analyser mode
 // (sklearn_analyser.py:52-69,103-107) or the raw centre in offline mode
-// (file_processing.py:51-66).  fp32 arithmetic; the reference's fp64 std is 0
-// exactly when all five values are equal (0/0 = NaN there), so that case is
-// tested explicitly instead of relying on fp32 rounding of the mean.
+// (file_processing.py:51-66).  fp32 arithmetic, except where a coefficient
+// is flat (all five values equal): there the reference's own fp64 formula on
+// these fp32 values -- mean = ((((x+x)+x)+x)+x)/5 is exact (every partial sum
+// of five floats fits a double), so x - mean = 0 and Mn = 0/0 = NaN, exactly
+// as numpy gives on these MFCCs; fp32 rounding of the mean could instead
+// leave a tiny non-zero std and a finite Mn, so flatness is tested
+// explicitly.  (The reference's MFCCs are fp64: on a digital-silence window
+// its fp64 5-sum rounds at some coefficients -- c4 and c7 of the 26-filter
+// silence MFCC -- and it gets Mn = +-1 there instead of NaN.  FFN labels are
+// unaffected -- any NaN feature makes the window class 0 in both -- but a
+// decision tree sees NaN where the reference sees +-1: DESIGN.md section 2.)
 struct Feat3 {
   float mn, d1, d2;
 };

@@ -562,7 +562,7 @@ __device__ __forceinline__ void lds_barrier() {
 // -DVAD_DIAG_BUILD=n`, never the shipped libvad_amd.so): 5/6 timestamps, 7 an
 // L2-resident source, 9 per-workgroup stamps, 10 phase 1 only -- outputs wrong.
 // HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
-template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0>
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0, bool WIN = false>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out) {
@@ -725,6 +725,22 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     v2f* gscr = scr + grp * kGroupScratch;
     LaneConsts L;
     lane_consts(plan, j, L);
+    // optional analysis window (plan->window, default off: not in the
+    // reference, mfcc.py:59-61): lane j's samples 32 n1 + 2 j, + 1
+    float wv[WIN ? 2 * NZ : 1];
+    if constexpr (WIN) {
+#pragma unroll
+      for (int n1 = 0; n1 < NZ; ++n1) {
+        wv[2 * n1] = plan->window[32 * n1 + 2 * j];
+        wv[2 * n1 + 1] = plan->window[32 * n1 + 2 * j + 1];
+      }
+    }
+    auto windowed = [&](v2f (&b)[NZ]) __attribute__((always_inline)) {
+      if constexpr (WIN) {
+#pragma unroll
+        for (int n1 = 0; n1 < NZ; ++n1) b[n1] = b[n1] * (v2f){wv[2 * n1], wv[2 * n1 + 1]};
+      }
+    };
     // software pipeline: the samples of the next pass are in flight while
     // the current pass computes
     v2f bufA[NZ], bufB[NZ];
@@ -808,6 +824,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         load_stage_a<TIN, NZ, VEC2, LEN, 8, NZ>(sb, len, j, bufB);
         __builtin_amdgcn_sched_barrier(0);
       } else if (work) {
+        windowed(bufA);
         stage_a<NZ, LEN>(bufA, len, L, j, u);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
@@ -819,6 +836,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           // overlap: pass 1's stage A covers the latency of pass 0's reads
           __builtin_amdgcn_sched_barrier(0);
           VAD_STAMP(2);
+          windowed(bufB);
           stage_a<NZ, LEN>(bufB, len, L, j, u);
           __builtin_amdgcn_sched_barrier(0);
           load_pass(tile + 1, 1, bufB);
@@ -830,6 +848,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           // variants within 256 VGPRs
           if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
           __builtin_amdgcn_sched_barrier(0);
+          windowed(bufB);
           stage_a<NZ, LEN>(bufB, len, L, j, u);
           __builtin_amdgcn_sched_barrier(0);
           load_pass(tile + 1, 1, bufB);
@@ -1104,7 +1123,7 @@ static int num_cus() {
 }
 
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0,
-          int HOPC = 0>
+          int HOPC = 0, bool WIN = false>
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
@@ -1113,10 +1132,10 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
   const size_t smem = mfcc_smem_bytes();
   static std::atomic<unsigned long long> attr_done{0};
   const hipError_t e = ensure_dyn_lds(
-      reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>), (int)smem,
+      reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC, WIN>), (int)smem,
       attr_done);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>), dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC, WIN>), dim3(grid), dim3(kThreads),
                      smem, st, plan, src, stride, len, n, out);
   return hipGetLastError();
 }
@@ -1127,6 +1146,13 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
   const int used = len < kFftN ? len : kFftN;
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
                     ((stride & 1) == 0) && ((used & 1) == 0);
+  if (spec == kSpecWindow) {  // optional analysis window: the runtime-table kernel with WIN
+    if (used <= 32 * 13)
+      return vec2 ? launch_t<TIN, MODE, 13, true, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
+                  : launch_t<TIN, MODE, 13, false, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
+    return vec2 ? launch_t<TIN, MODE, 16, true, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
+                : launch_t<TIN, MODE, 16, false, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
+  }
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
       if constexpr (VAD_DIAG_BUILD != 0) {  // diagnostic library builds only (outputs wrong)
@@ -1162,9 +1188,11 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src
   if (n <= 0) return hipSuccess;
   switch (mode) {
     case kAudioToMfcc: return launch_m<float, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
-    case kAudioToSpec: return launch_m<float, kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
+    case kAudioToSpec:
+      return launch_m<float, kAudioToSpec>(plan, spec == kSpecWindow ? kSpecWindow : 0, src, stride, len, n, out, st);
     default:
       if (spec == 1) return launch_t<float, kSpecToMfcc, 13, false, 0, 1>(plan, src, 0, 0, n, out, st);
+      if (spec == kSpecWindow) spec = 0;  // spectra in: the window was applied before the FFT
       if (spec == 2) return launch_t<float, kSpecToMfcc, 13, false, 0, 2>(plan, src, 0, 0, n, out, st);
       return launch_t<float, kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
   }
@@ -1173,7 +1201,8 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src
 hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_t* src,
                            int64_t stride, int len, int64_t n, float* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (mode == kAudioToSpec) return launch_m<int16_t, kAudioToSpec>(plan, 0, src, stride, len, n, out, st);
+  if (mode == kAudioToSpec)
+    return launch_m<int16_t, kAudioToSpec>(plan, spec == kSpecWindow ? kSpecWindow : 0, src, stride, len, n, out, st);
   return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
 }
 

@@ -49,4 +49,43 @@ hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const flo
   return hipGetLastError();
 }
 
+// Optional pre-emphasis (not in the reference pipeline, mfcc.py:59-61; the
+// python_speech_features convention): y[0] = x[0], y[t] = x[t] - a x[t-1]
+// along each row (a whole clip is one row).  Elementwise, 16-B vector loads
+// of four samples plus the one before them; out of place.
+__global__ __launch_bounds__(256) void preemphasis_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                          int64_t n_rows, int64_t row_len, int64_t stride,
+                                                          float a) {
+#pragma clang fp contract(off)  // a rounded product, then the difference: numpy's two roundings
+  const int64_t quads = (row_len + 3) / 4;
+  const int64_t total = n_rows * quads;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / quads, q = i - r * quads;
+    const float* xr = x + r * stride;
+    float* yr = y + r * stride;
+    const int64_t t0 = 4 * q;
+    float prev = t0 > 0 ? xr[t0 - 1] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t t = t0 + k;
+      if (t < row_len) {
+        const float v = xr[t];
+        yr[t] = t == 0 ? v : v - a * prev;
+        prev = v;
+      }
+    }
+  }
+}
+
+hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,
+                              hipStream_t st) {
+  if (n_rows <= 0 || row_len <= 0) return hipSuccess;
+  int64_t blocks = (n_rows * ((row_len + 3) / 4) + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(preemphasis_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n_rows, row_len, stride,
+                     a);
+  return hipGetLastError();
+}
+
 }  // namespace vad

@@ -33,7 +33,11 @@ struct MfccDev {
   float dct[kMaxCoefs * kMaxFilters];  // lifter(L) x DCT-II ortho, [c][m]
   float2 tw_a[256];                  // W256^(n2*k1), [n2][k1]
   float2 tw_b[256];                  // W512^k
+  float window[kFftN];               // optional analysis window (kSpecWindow plans), 0 past the frame
 };
+
+// plan variant of a plan with an analysis window (vad_mfcc_plan_set_window)
+constexpr int kSpecWindow = 3;
 
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -92,6 +96,8 @@ hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring
                              int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st);
 hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const float* hop, int64_t hstride,
                               int hlen, int64_t n_streams, hipStream_t st);
+hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,
+                              hipStream_t st);
 hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
                            hipStream_t st);
 hipError_t launch_simple_features(const float* frames, int64_t n_frames, int frame_len,

@@ -16,7 +16,7 @@ import torch
 from . import _lib
 from .config import MfccConfig
 from .ffn import FFNClassifier
-from .plan import MfccPlan, check_out, n_frames, window_features
+from .plan import MfccPlan, check_out, n_frames, preemphasis, window_features
 
 
 def split_into_frames(data, frame_size, step, transcription_path=None, frame_rate=None):
@@ -49,9 +49,18 @@ class VadPipeline:
     def n_frames(self, n_samples):
         return n_frames(n_samples, self.cfg.frame_size, self.cfg.hop)
 
+    def _staged(self, audio, stream=None):
+        """The clip after the optional pre-emphasis (cfg.preemph; off by default)."""
+        if self.cfg.preemph is None:
+            return audio
+        if audio.dtype != torch.float32:
+            audio = audio.float()
+        return preemphasis(audio, self.cfg.preemph, stream=stream)
+
     def mfcc(self, audio, out=None, stream=None):
         """(F, n_mfcc) MFCCs of every frame of a device clip."""
-        return self.plan.clip_mfcc(audio, self.cfg.frame_size, self.cfg.hop, out=out, stream=stream)
+        return self.plan.clip_mfcc(self._staged(audio, stream), self.cfg.frame_size, self.cfg.hop, out=out,
+                                   stream=stream)
 
     def features(self, audio, mode=None, stream=None):
         """(F-5, 3*n_mfcc) feature rows of a device clip."""
@@ -103,6 +112,7 @@ class VadPipeline:
                 raise ValueError("the fused kernel runs the FFN classifiers only")
             return self.ffn.window_labels(self.mfcc(audio, stream=stream), self.mode, out=out,
                                           stream=stream)
+        audio = self._staged(audio, stream)
         ws = None if fused else self._workspace(self.workspace_bytes(audio.numel()), audio.device, stream)
         fn = "vad_mfcc_ffn" if audio.dtype == torch.float32 else "vad_mfcc_ffn_i16"
         _lib.check(getattr(_lib.lib(), fn)(

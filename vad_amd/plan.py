@@ -80,7 +80,22 @@ class MfccPlan:
     def from_config(cls, cfg: MfccConfig = MfccConfig()):
         from .mfcc import get_mel_filterbanks
         fb = get_mel_filterbanks(cfg.low_hz, cfg.high_hz, cfg.fft_n, cfg.n_filters, cfg.sample_rate)
-        return cls(fb, cfg.n_mfcc, cfg.fft_n, cfg.lifter)
+        plan = cls(fb, cfg.n_mfcc, cfg.fft_n, cfg.lifter)
+        if cfg.window is not None:
+            if cfg.window != "hamming":
+                raise ValueError(f"unknown window {cfg.window!r} (None or 'hamming')")
+            plan.set_window(np.hamming(cfg.frame_size))
+        return plan
+
+    def set_window(self, window):
+        """Multiply every frame by `window` (<= 512 samples) before the FFT --
+        an optional stage the reference does not have; None removes it."""
+        if window is None:
+            check(lib().vad_mfcc_plan_set_window(self._h, None, 0), "vad_mfcc_plan_set_window")
+            return
+        w = np.ascontiguousarray(np.asarray(window, np.float32).reshape(-1))
+        check(lib().vad_mfcc_plan_set_window(self._h, w.ctypes.data_as(ctypes.c_void_p), w.size),
+              "vad_mfcc_plan_set_window")
 
     @property
     def handle(self):
@@ -223,6 +238,18 @@ class FfnPlan:
         check(lib().vad_features_ffn(self._h, ptr(mfcc), f, c, int(mode), ptr(out),
                                      stream_ptr(stream)), "vad_features_ffn")
         return out
+
+
+def preemphasis(x, coeff, out=None, stream=None):
+    """y[0] = x[0], y[t] = x[t] - coeff x[t-1] of a device fp32 clip (1-D) or
+    of every row of a frame matrix (2-D): an optional stage, not in the
+    reference."""
+    _require_cuda_tensor(x, "x")
+    rows, n = (1, x.numel()) if x.dim() == 1 else tuple(x.shape)
+    out = _out(out, tuple(x.shape), torch.float32, x.device)
+    check(lib().vad_preemphasis_f32(ptr(x), ptr(out), rows, n, n, ctypes.c_float(coeff), stream_ptr(stream)),
+          "vad_preemphasis_f32")
+    return out
 
 
 def window_logits(ffn_plan, mfcc, mode=_lib.FEAT_ANALYSER, stream=None):

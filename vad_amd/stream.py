@@ -26,6 +26,8 @@ class StreamBatch:
     def __init__(self, n_streams, ffn, cfg: MfccConfig = MfccConfig(), device=None):
         if not isinstance(ffn, FFNClassifier):
             ffn = FFNClassifier(ffn)
+        if cfg.preemph is not None:
+            raise ValueError("pre-emphasis is a clip-level stage (VadPipeline); streams take raw frames")
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
         self.cfg, self.ffn, self.n = cfg, ffn, int(n_streams)
         self.plan = MfccPlan.from_config(cfg)
