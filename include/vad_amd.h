@@ -274,6 +274,15 @@ int64_t vad_stream_ring_floats(int64_t n_streams, int32_t mfcc_n);
  * live loop of vad.py:37-49 hands to feed_frame.  One kernel; capturable. */
 int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, const float* hop,
                         int64_t hop_stride, int32_t hop_len, int64_t n_streams, void* stream);
+/* One hop of every stream in ONE kernel (one wave per stream): advance the
+ * frame buffer by the hop (as vad_stream_push_hop), 512-point FFT of the new
+ * frame, mel / log10 / lifter x DCT, classify the ring's window, push the
+ * new MFCC row (as vad_stream_step) -- the FFN forward in exact f32 on the
+ * VALU, one output unit per lane.  The hipGraph-free, latency-first form of
+ * push_hop + step for many small batches (BASELINE config 5). */
+int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
+                   int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
+                   float* ring, int32_t* count, uint8_t* labels, void* stream);
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);

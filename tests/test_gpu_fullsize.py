@@ -114,7 +114,8 @@ def test_c3_full_clip_vs_oracle(torch_cuda):
     assert np.isnan(x).any(axis=1).sum() > 0  # digital silence exercised
 
 
-def test_c5_512_streams_graph_replay(torch_cuda, golden):
+@pytest.mark.parametrize("kernel", ["hop", "three"])
+def test_c5_512_streams_graph_replay(torch_cuda, golden, kernel):
     """C5: 512 concurrent streams, 40 hops of 10 ms each as hipGraph replays
     (frame assembly + MFCC + features + FFN), every stream's labels vs the
     oracle's feed_frame semantics on that stream's audio."""
@@ -125,7 +126,7 @@ def test_c5_512_streams_graph_replay(torch_cuda, golden):
     layers = [(w[f"ref39_W{i}"], w[f"ref39_b{i}"]) for i in range(4)]
     S, T = 512, 40
     clips = np.stack([O.synth_clip(160 * (T - 1) + 401, seed=500 + s) for s in range(S)])
-    sb = StreamBatch(S, FFNClassifier(layers))
+    sb = StreamBatch(S, FFNClassifier(layers), kernel=kernel)
     sb.prime(torch.from_numpy(np.ascontiguousarray(clips[:, :240])).cuda())
     sb.capture()
     hops = torch.from_numpy(np.ascontiguousarray(
@@ -139,6 +140,14 @@ def test_c5_512_streams_graph_replay(torch_cuda, golden):
         ref_l.append(O.ffn_labels(x, layers))
         marg.append(O.ffn_margin(x, layers))
     ref_l, marg = np.stack(ref_l), np.stack(marg)  # (S, T-5)
+    # the MFCC ring the streams hold equals the oracle's last five frames
+    ring = sb.ring.cpu().numpy()
+    cnt = sb.count.cpu().numpy()
+    for s in range(0, S, 37):
+        want = O.mfcc_batch(clips[s], fb)[-5:]
+        got_rows = np.stack([ring[s][(cnt[s] + d) % 5] for d in range(5)])
+        rel = np.linalg.norm(got_rows - want, axis=1) / np.linalg.norm(want, axis=1)
+        assert rel.max() <= MFCC_TOL, (s, rel.max())
     sure = marg > LABEL_MARGIN
     np.testing.assert_array_equal(got[:, 5:][sure], ref_l[sure])
     assert int((got[:, 5:] != ref_l).sum()) <= 2

@@ -68,6 +68,8 @@ SIGNATURES = {
     "vad_mfcc_ffn_fusable": (c_i32, [c_vp, c_vp, c_i32, c_i32]),
     "vad_stream_ring_floats": (c_i64, [c_i64, c_i32]),
     "vad_stream_push_hop": (c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp]),
+    "vad_stream_hop": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp,
+                               c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                 c_vp]),
     "vad_rccl_available": (c_int, []),

@@ -19,6 +19,9 @@ struct vad_mfcc_plan {
   int spec;          // 1/2: equals the compile-time Mel26/Mel40 tables bit for bit;
                      // kSpecWindow: an analysis window is set
   int table_spec;    // the compile-time table match without a window
+  float* hop_blob;   // stream_hop_kernel's tables, one contiguous block (LDS-staged per launch)
+  int hop_blob_n;    // floats (a multiple of 4)
+  int n_taps;
 };
 
 // Does the runtime plan equal compile-time table T (taps, ranges, DCT rows)?
@@ -43,6 +46,7 @@ struct vad_ffn_plan {
   FfnDev net;        // by-value kernel argument, frag -> device buffer
   float* frag_dev;
   uint32_t* fragh_dev;  // split-f16 weights (null when the topology has none)
+  float* wraw_dev;      // the weights as given (streaming hop kernel)
 };
 
 #define VAD_TRY(x)                          \
@@ -126,10 +130,25 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
   }
   p->spec = p->table_spec = matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
-  hipError_t e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
-  if (e != hipSuccess) { free(p); return (int)e; }
+  // the streaming hop kernel's tables as one block: W512^k (256 complex),
+  // f_lo / f_len / f_off (as int bits), the taps, the DCT rows at stride nf
+  p->n_taps = off;
+  std::vector<float> blob;
+  for (int k = 0; k < 256; ++k) { blob.push_back(h.tw_b[k].x); blob.push_back(h.tw_b[k].y); }
+  for (const int* arr : {h.f_lo, h.f_len, h.f_off})
+    for (int m = 0; m < n_filters; ++m) { float f; memcpy(&f, &arr[m], 4); blob.push_back(f); }
+  blob.insert(blob.end(), h.taps, h.taps + off);
+  for (int c = 0; c < mfcc_n; ++c)
+    for (int m = 0; m < n_filters; ++m) blob.push_back(h.dct[c * kMaxFilters + m]);
+  while (blob.size() % 4) blob.push_back(0.f);
+  p->hop_blob_n = (int)blob.size();
+  hipError_t e = hipMalloc((void**)&p->hop_blob, blob.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(p->hop_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->hop_blob); free(p); return (int)e; }
+  e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
+  if (e != hipSuccess) { (void)hipFree(p->hop_blob); free(p); return (int)e; }
   e = hipMemcpy(p->dev, &h, sizeof(MfccDev), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(p->dev); free(p); return (int)e; }
+  if (e != hipSuccess) { (void)hipFree(p->dev); (void)hipFree(p->hop_blob); free(p); return (int)e; }
   *out = p;
   return VAD_OK;
 }
@@ -137,6 +156,7 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
 int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
   if (!p) return VAD_OK;
   (void)hipFree(p->dev);
+  (void)hipFree(p->hop_blob);
   free(p);
   return VAD_OK;
 }
@@ -318,12 +338,27 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
     }
   }
 
+  // the weights as given: W_l (in, out) row-major, then b_l
+  std::vector<float> wraw;
+  for (int l = 0; l < n_layers; ++l) {
+    net.woff[l] = (int)wraw.size();
+    wraw.insert(wraw.end(), W[l], W[l] + (size_t)dims[l] * dims[l + 1]);
+    net.boff[l] = (int)wraw.size();
+    wraw.insert(wraw.end(), b[l], b[l] + dims[l + 1]);
+  }
+  while (wraw.size() % 4) wraw.push_back(0.f);  // whole 16-B vectors for the LDS staging
+  net.wraw_n = (int)wraw.size();
+
   vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));
   if (!p) return VAD_ENOMEM;
-  hipError_t e = hipMalloc((void**)&p->frag_dev, frag.size() * sizeof(float));
+  hipError_t e = hipMalloc((void**)&p->wraw_dev, wraw.size() * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(p->wraw_dev, wraw.data(), wraw.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (e != hipSuccess) { (void)hipFree(p->wraw_dev); free(p); return (int)e; }
+  net.wraw = p->wraw_dev;
+  e = hipMalloc((void**)&p->frag_dev, frag.size() * sizeof(float));
   if (e != hipSuccess) { free(p); return (int)e; }
   e = hipMemcpy(p->frag_dev, frag.data(), frag.size() * sizeof(float), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(p->frag_dev); free(p); return (int)e; }
+  if (e != hipSuccess) { (void)hipFree(p->frag_dev); (void)hipFree(p->wraw_dev); free(p); return (int)e; }
   net.frag = p->frag_dev;
   net.fragh = nullptr;
   if (!fragh.empty()) {
@@ -333,6 +368,7 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
     if (e != hipSuccess) {
       (void)hipFree(p->fragh_dev);
       (void)hipFree(p->frag_dev);
+      (void)hipFree(p->wraw_dev);
       free(p);
       return (int)e;
     }
@@ -359,6 +395,7 @@ int vad_ffn_plan_destroy(vad_ffn_plan* p) {
   if (!p) return VAD_OK;
   (void)hipFree(p->frag_dev);
   if (p->fragh_dev) (void)hipFree(p->fragh_dev);
+  (void)hipFree(p->wraw_dev);
   free(p);
   return VAD_OK;
 }
@@ -594,6 +631,20 @@ int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, 
   if (!frames || !hop) return VAD_EINVAL;
   return (int)launch_stream_push(frames, frame_stride, frame_len, hop, hop_stride, hop_len, n_streams,
                                  (hipStream_t)stream);
+}
+
+int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
+                   int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
+                   float* ring, int32_t* count, uint8_t* labels, void* stream) {
+  if (!plan || !ffn || n_streams < 0 || frame_len <= 0 || frame_len > 1024 || hop_len <= 0 ||
+      hop_len > frame_len || frame_stride < frame_len || hop_stride < hop_len)
+    return VAD_EINVAL;
+  if (n_streams == 0) return VAD_OK;
+  if (!frames || !hop || !ring || !count || !labels) return VAD_EINVAL;
+  if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  return (int)launch_stream_hop(plan->dev, plan->hop_blob, plan->hop_blob_n, plan->host.n_filters, plan->n_taps,
+                                ffn->net, frames, frame_stride, frame_len, hop, hop_stride, hop_len,
+                                n_streams, plan->host.mfcc_n, ring, count, labels, (hipStream_t)stream);
 }
 
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,

@@ -359,15 +359,6 @@ __device__ __forceinline__ void finish_b(const LaneConsts& L, v2f (&col)[32],
   for (int m = 4; m < 8; ++m) po4[-32 * m] = pnv[m];
 }
 
-// log10 of a positive energy: native v_log_f32 (with a pre-scale for tiny
-// inputs) times log10(2) -- ~1e-7 relative, far inside the 1e-4 budget.
-__device__ __forceinline__ float log10_pos(float e) {
-  const bool tiny = e < 0x1p-100f;
-  const float x = tiny ? e * 0x1p64f : e;
-  const float l2 = __builtin_amdgcn_logf(x);  // log2
-  return fmaf(l2, 0.30102999566398120f, tiny ? -19.26591972249479649f : 0.f);
-}
-
 // Log-mel rows of a tile, [64][LMS] fp32: LMS is 4 x odd, so the
 // frame-per-lane ds_read_b128 of phase 2b hits disjoint banks.
 template <int SPEC>

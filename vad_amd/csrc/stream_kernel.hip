@@ -10,6 +10,8 @@
 // beyond anything store i writes -- so no sample is overwritten before it is
 // read.
 #include "vad_common.h"
+#include "features.h"
+#include "ffn_dev.h"
 
 namespace vad {
 
@@ -85,6 +87,304 @@ hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t 
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(preemphasis_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n_rows, row_len, stride,
                      a);
+  return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// One analyser hop of every stream in ONE kernel, one wave per stream
+// (BASELINE config 5: many small batches, latency first).  The clip kernels
+// spread a 64-frame tile over a workgroup; a hop brings one frame per
+// stream, so here each wave owns its stream end to end:
+//   frame    advance the 400-sample buffer by the hop (as stream_push_kernel)
+//   FFT      z[n] = x[2n] + i x[2n+1] (zero past min(len, 512)), 256-point
+//            Stockham radix-4 (4 stages through wave-private LDS, lane j
+//            one butterfly per stage), then the real-FFT split into
+//            |2X[k]|^2, k = 0..255 (the 2^-20 of |X/512|^2 sits in the taps)
+//   mel      lane m: filter m's taps, (==0 -> eps), log10 (mfcc.py:72-75)
+//   DCT      lane c: lifter x DCT-II ortho row c (mfcc.py:76-78)
+//   window   the ring's five rows in arrival order -> analyser features
+//            (sklearn_analyser.py:52-69), classified if the stream has seen
+//            five frames, then the new row pushed (:71-74)
+//   FFN      exact f32 on the VALU, lane o = output unit o, weights as given
+//            (ffn_trainer.py:106-116), NaN-keeping ReLU, np.argmax rules.
+// Lanes within the wave exchange through LDS only (in order per wave): no
+// workgroup barrier anywhere.
+// ---------------------------------------------------------------------------
+// Per-wave LDS scratch (floats): the FFT's ping-pong buffers (the power
+// row reuses the first once the transform is done), the log-mel row, two
+// activation rows.
+#ifndef VAD_HOP_DIAG
+#define VAD_HOP_DIAG 0  // diagnostic builds only: stop after 1 staging, 2 FFT, 3 mel / DCT, 4 features
+#endif
+constexpr int kHopZ = 2 * 256;                     // one 256-point complex buffer
+constexpr int kHopWaveFloats = 2 * kHopZ + kMaxFilters + 64 + 64;
+
+// Block-shared LDS, staged once per block from the plans (the per-stream
+// chain would otherwise wait on one L2 round trip per tap, DCT term and
+// weight): twiddles, filter ranges and taps, the DCT rows, the FFN weights.
+struct HopTables {
+  const float2* tw;  // W512^k, k < 256
+  const int* f_lo;
+  const int* f_len;
+  const int* f_off;
+  const float* taps;
+  const float* dct;  // [c][m], stride nf
+  const float* w;    // the FFN weights as given (FfnDev::wraw layout)
+};
+
+__device__ __forceinline__ float2 cmulf(float2 a, float2 w) {
+  return make_float2(fmaf(a.x, w.x, -a.y * w.y), fmaf(a.x, w.y, a.y * w.x));
+}
+
+// W256^m, 0 <= m < 256, from the W512^k table
+__device__ __forceinline__ float2 w256(const float2* __restrict__ tw, int m) {
+  const float2 t = tw[2 * (m & 127)];
+  return m < 128 ? t : make_float2(-t.x, -t.y);
+}
+
+__global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restrict__ blob, int blob_n, int nf,
+                                                          int n_taps, FfnDev net,
+                                                          float* __restrict__ frames, int64_t fstride, int len,
+                                                          const float* __restrict__ hop, int64_t hstride,
+                                                          int hlen, int64_t n_streams, int mfcc_n,
+                                                          float* __restrict__ ring, int* __restrict__ count,
+                                                          uint8_t* __restrict__ labels) {
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  const int waves = blockDim.x >> 6;
+  // -- stage the plans' tables (the MFCC plan's hop blob, then the FFN
+  // weights) with 16-B loads, all issued before any store: one L2 round
+  // trip, then the block's only barrier
+  float* base = hsm + waves * kHopWaveFloats;
+  {
+    const float4* m4 = reinterpret_cast<const float4*>(blob);
+    const float4* w4 = reinterpret_cast<const float4*>(net.wraw);
+    float4* d4 = reinterpret_cast<float4*>(base);
+    const int nm4 = blob_n >> 2, n4 = nm4 + (net.wraw_n >> 2);
+    for (int i0 = 0; i0 < n4; i0 += 4 * (int)blockDim.x) {
+      float4 t[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * blockDim.x + threadIdx.x;
+        t[q] = i < nm4 ? m4[i] : (i < n4 ? w4[i - nm4] : make_float4(0.f, 0.f, 0.f, 0.f));
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = i0 + q * blockDim.x + threadIdx.x;
+        if (i < n4) d4[i] = t[q];
+      }
+    }
+  }
+  HopTables T;
+  T.tw = reinterpret_cast<const float2*>(base);
+  const int* ilo = reinterpret_cast<const int*>(base + 2 * 256);
+  T.f_lo = ilo;
+  T.f_len = ilo + nf;
+  T.f_off = ilo + 2 * nf;
+  T.taps = base + 2 * 256 + 3 * nf;
+  T.dct = T.taps + n_taps;
+  T.w = base + blob_n;
+
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int64_t s = (int64_t)blockIdx.x * waves + wv;
+  // -- frame: shift by the hop, append the new samples (stream_push_kernel);
+  // issued before the barrier, so their latency overlaps the staging
+  float* row = frames + (s < n_streams ? s : 0) * fstride;
+  const float* hs = hop + (s < n_streams ? s : 0) * hstride;
+  const int keep = len - hlen;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int t = lane + 64 * i;
+    v[i] = t < keep ? row[t + hlen] : (t < len ? hs[t - keep] : 0.f);
+  }
+  // the stream's frame count and MFCC ring, requested now too (the window
+  // needs them only after the FFT)
+  const int64_t sc = s < n_streams ? s : 0;
+  const int c = count[sc];
+  float* rs = ring + sc * 5 * mfcc_n;
+  float rv[5];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) rv[d] = lane < mfcc_n ? rs[d * mfcc_n + lane] : 0.f;
+  __syncthreads();
+  if (s >= n_streams) return;  // wave-uniform; no barrier below
+  if (VAD_HOP_DIAG == 1) {
+    if (lane == 0) labels[s] = (uint8_t)v[0];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int t = lane + 64 * i;
+    if (t < len) row[t] = v[i];
+  }
+  float* scr = hsm + wv * kHopWaveFloats;
+  float2* z0 = reinterpret_cast<float2*>(scr);
+  float2* z1 = reinterpret_cast<float2*>(scr + kHopZ);
+  float* lmr = scr + 2 * kHopZ;
+  float* act_a = lmr + kMaxFilters;
+  float* act_b = act_a + 64;
+  // samples of the FFT (np.fft.fft(x, 512): zero-pad / truncate, mfcc.py:61)
+  const int used = len < kFftN ? len : kFftN;
+  float* xs = reinterpret_cast<float*>(z1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int t = lane + 64 * i;
+    xs[t] = t < used ? v[i] : 0.f;
+  }
+  // LDS is in order within a wave; these keep the compiler from moving
+  // accesses of one phase (other lanes' data, other element types) across
+  // the next
+  asm volatile("" ::: "memory");
+
+  // -- 256-point complex FFT, Stockham radix-4
+  float2* src = z1;
+  float2* dst = z0;
+#pragma unroll
+  for (int st = 0; st < 4; ++st) {
+    const int ns = 1 << (2 * st);  // 1, 4, 16, 64
+    const int k = lane & (ns - 1);
+    float2 a0 = src[lane], a1 = src[lane + 64], a2 = src[lane + 128], a3 = src[lane + 192];
+    if (st > 0) {
+      const int m = k * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
+      a1 = cmulf(a1, w256(T.tw, m));
+      a2 = cmulf(a2, w256(T.tw, 2 * m));
+      a3 = cmulf(a3, w256(T.tw, 3 * m));
+    }
+    const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
+    const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
+    const int o = (lane >> (2 * st)) * (4 * ns) + k;
+    dst[o] = make_float2(b0.x + b2.x, b0.y + b2.y);
+    dst[o + ns] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
+    dst[o + 2 * ns] = make_float2(b0.x - b2.x, b0.y - b2.y);
+    dst[o + 3 * ns] = make_float2(b1.x - b3.y, b1.y + b3.x);  // b1 + i b3
+    float2* t = src;
+    src = dst;
+    dst = t;
+    asm volatile("" ::: "memory");
+  }
+  if (VAD_HOP_DIAG == 2) {
+    if (lane == 0) labels[s] = (uint8_t)src[3].x;
+    return;
+  }
+  // -- real-FFT split: 2X[k] = S - i W512^k D, S = Z[k] + conj(Z[-k]),
+  // D = Z[k] - conj(Z[-k]); |2X|^2 into the free buffer
+  float* pw = reinterpret_cast<float*>(dst);
+  float pk[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = lane + 64 * q;
+    const float2 zk = src[k], zn = src[(256 - k) & 255];
+    const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
+    const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
+    const float2 Tw = cmulf(D, T.tw[k]);
+    const float u = S.x + Tw.y, vv = S.y - Tw.x;
+    pk[q] = fmaf(u, u, vv * vv);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pw[lane + 64 * q] = pk[q];
+  asm volatile("" ::: "memory");
+  // -- mel + log10 (lane m), lifter x DCT (lane c)
+  if (lane < nf) {
+    const int lo = T.f_lo[lane], n = T.f_len[lane];
+    const float* wt = T.taps + T.f_off[lane];
+    // unrolled: the LDS reads of a batch are in flight together (a rolled
+    // loop waits one LDS round trip per tap)
+    float e = 0.f;
+#pragma unroll 8
+    for (int t = 0; t < n; ++t) e = fmaf(wt[t], pw[lo + t], e);
+    lmr[lane] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
+  }
+  asm volatile("" ::: "memory");
+  float mf = 0.f;
+  if (lane < mfcc_n) {
+    const float* d = T.dct + lane * nf;
+#pragma unroll 8
+    for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
+  }
+
+  if (VAD_HOP_DIAG == 3) {
+    if (lane == 0) labels[s] = (uint8_t)mf;
+    return;
+  }
+  // -- window of the five previous frames, then push the new row
+  const bool have = c >= 5;
+  if (lane < mfcc_n) {
+    if (have) {
+      // slot (c + d) % 5, d = 0..4: the ring in arrival order, oldest first
+      float r[5];
+#pragma unroll
+      for (int d = 0; d < 5; ++d) {
+        const int q = (c + d) % 5;
+        r[d] = q == 0 ? rv[0] : q == 1 ? rv[1] : q == 2 ? rv[2] : q == 3 ? rv[3] : rv[4];
+      }
+      const Feat3 ft = feature_triple(r[0], r[1], r[2], r[3], r[4], VAD_FEAT_ANALYSER);
+      act_a[lane] = ft.mn;
+      act_a[mfcc_n + lane] = ft.d1;
+      act_a[2 * mfcc_n + lane] = ft.d2;
+    }
+    rs[(c % 5) * mfcc_n + lane] = mf;
+  }
+  asm volatile("" ::: "memory");
+  uint8_t label = 255;
+  if (have && VAD_HOP_DIAG != 4) {
+    // -- FFN: exact f32, lane o of each layer
+    float* hin = act_a;
+    float* hout = act_b;
+    const int nl = net.n_layers;
+    for (int l = 0; l < nl; ++l) {
+      const int din = net.dims[l], dout = net.dims[l + 1];
+      if (lane < dout) {
+        const float* W = T.w + net.woff[l];
+        float acc = T.w[net.boff[l] + lane];
+#pragma unroll 8
+        for (int k = 0; k < din; ++k) acc = fmaf(W[k * dout + lane], hin[k], acc);
+        hout[lane] = l + 1 < nl ? relu_nan(acc) : acc;
+      }
+      float* t = hin;
+      hin = hout;
+      hout = t;
+      asm volatile("" ::: "memory");
+    }
+    const f32x4 zl = {hin[0], hin[1 < net.n_classes ? 1 : 0], hin[2 < net.n_classes ? 2 : 0],
+                      hin[3 < net.n_classes ? 3 : 0]};
+    label = (uint8_t)argmax_classes(zl, net.n_classes);
+  }
+  if (lane == 0) {
+    labels[s] = label;
+    count[s] = (c + 1 >= 10) ? c + 1 - 5 : c + 1;
+  }
+}
+
+hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n, int nf, int n_taps,
+                             const FfnDev& net, float* frames, int64_t fstride, int len, const float* hop,
+                             int64_t hstride, int hlen, int64_t n_streams, int mfcc_n, float* ring, int* count,
+                             uint8_t* labels, hipStream_t st) {
+  (void)plan;
+  if (n_streams <= 0) return hipSuccess;
+  const size_t tables = (size_t)(blob_n + net.wraw_n) * sizeof(float);
+  // streams per block: spread over every CU first (each block stages the
+  // ~26 KB of tables from L2 once; the per-stream chain is LDS-bound, so
+  // fewer waves per CU run it faster), up to 16 waves when there are more
+  // streams than CUs, and as many as the LDS holds
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+      n_cu = 256;
+  }
+  int waves = 1;
+  while (waves < 16 && (int64_t)waves * n_cu < n_streams) waves <<= 1;
+  while (waves > 1 && tables + (size_t)waves * kHopWaveFloats * sizeof(float) > 160 * 1024) waves >>= 1;
+  const size_t smem = tables + (size_t)waves * kHopWaveFloats * sizeof(float);
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  static std::atomic<unsigned long long> attr_done{0};
+  const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&stream_hop_kernel), 160 * 1024, attr_done);
+  if (e != hipSuccess) return e;
+  const dim3 grid((unsigned)((n_streams + waves - 1) / waves));
+  hipLaunchKernelGGL(stream_hop_kernel, grid, dim3(64 * waves), smem, st, blob, blob_n, nf, n_taps, net, frames,
+                     fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels);
   return hipGetLastError();
 }
 

@@ -56,6 +56,12 @@ struct FfnDev {
   // optional (tests): the fp32 logits of every classified row,
   // logits[row * n_classes + c] (null: labels only)
   float* logits;
+  // the Keras weights as given (W_l (in, out) row-major, then b_l), for the
+  // one-wave-per-stream VALU forward of the streaming hop kernel
+  const float* wraw;
+  int wraw_n;  // floats in wraw
+  int woff[VAD_MAX_FFN_LAYERS];
+  int boff[VAD_MAX_FFN_LAYERS];
 };
 
 // Decision-tree node (tree_kernel.hip): internal if feature >= 0 (go left
@@ -94,6 +100,10 @@ hipError_t launch_ffn(const FfnDev& net, int src, const float* in, int64_t n_row
                       int mode, uint8_t* labels, hipStream_t st);
 hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring, int* count,
                              int64_t n_streams, int mfcc_n, uint8_t* labels, hipStream_t st);
+hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n, int nf, int n_taps,
+                             const FfnDev& net, float* frames, int64_t fstride, int len,
+                             const float* hop, int64_t hstride, int hlen, int64_t n_streams, int mfcc_n,
+                             float* ring, int* count, uint8_t* labels, hipStream_t st);
 hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const float* hop, int64_t hstride,
                               int hlen, int64_t n_streams, hipStream_t st);
 hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,
@@ -123,6 +133,15 @@ inline hipError_t ensure_dyn_lds(const void* fn, int bytes, std::atomic<unsigned
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
   if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
   return e;
+}
+
+// log10 of a positive energy: native v_log_f32 (with a pre-scale for tiny
+// inputs) times log10(2) -- ~1e-7 relative, far inside the 1e-4 budget.
+__device__ __forceinline__ float log10_pos(float e) {
+  const bool tiny = e < 0x1p-100f;
+  const float x = tiny ? e * 0x1p64f : e;
+  const float l2 = __builtin_amdgcn_logf(x);  // log2
+  return fmaf(l2, 0.30102999566398120f, tiny ? -19.26591972249479649f : 0.f);
 }
 
 // NaN-keeping ReLU (numpy / Keras keep NaN; fmaxf would drop it).
