@@ -215,6 +215,61 @@ def feed_frame_latency(dev, calls=2000, warm=50):
                                 "(not re-measured here: the reference cannot travel to the GPU box)"}
 
 
+def secondary_configs(dev, reps=60):
+    """The other BASELINE configs beside the headline (rank 0, N = 1):
+    C2 (configs[1]) MFCC only, 100k frames, 40 and 26 mel: six clips rotated
+    per launch (384 MB, past the 256 MiB Infinity Cache), HIP events around
+    `reps` launches; C5 (configs[4]) 512 analyser streams, one 10 ms hop per
+    step: the single-kernel hop and the three-kernel hipGraph replay."""
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.stream import StreamBatch
+    out = {}
+    F = 100_000
+    clips = [synth_audio(160 * (F - 1) + 401, 10 + i, dev) for i in range(6)]
+    mf = torch.empty((F, 13), dtype=torch.float32, device=dev)
+    for nf in (40, 26):
+        pipe = VadPipeline(cfg=MfccConfig(n_filters=nf))
+        for k in range(60):
+            pipe.mfcc(clips[k % 6], out=mf)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for k in range(reps):
+            pipe.mfcc(clips[k % 6], out=mf)
+        e.record()
+        torch.cuda.synchronize()
+        t = s.elapsed_time(e) / reps * 1e-3
+        out[f"c2_mfcc_100k_{nf}mel"] = {
+            "frames_per_s": F / t, "avg_launch_us": t * 1e6,
+            "achieved_GBps": MFCC_BYTES_PER_FRAME * F / t / 1e9,
+            "frac_hbm": MFCC_BYTES_PER_FRAME * F / t / 1e9 / HBM_PEAK_GBS,
+            "note": "6 rotated 64 MB clips (384 MB working set)"}
+    del clips
+    S = 512
+    for name, kernel, graph in (("hop_kernel", "hop", False), ("three_kernel_hipgraph", "three", True)):
+        sb = StreamBatch(S, FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)), kernel=kernel)
+        g = torch.Generator(device=dev).manual_seed(500)
+        sb.prime(torch.randn((S, 240), generator=g, device=dev) * 1000)
+        hops = [torch.randn((S, 160), generator=g, device=dev) * 1000 for _ in range(8)]
+        if graph:
+            sb.capture()
+        for k in range(200):
+            sb.step(hops[k % 8])
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for k in range(400):
+            sb.step(hops[k % 8])
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / 400 * 1e3
+        out[f"c5_512_streams_{name}"] = {"us_per_hop": us, "stream_frames_per_s": S / (us * 1e-6),
+                                         "x_real_time": 10_000.0 / us}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,6 +278,7 @@ def main():
     ap.add_argument("--frames", type=int, default=1_000_000)
     ap.add_argument("--ffn", default="bl13", choices=["bl13", "ref39"])
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")  # skip the C2 / C5 lines (profiling runs)
     # a GPU that was idle starts at low clocks and ramps for ~30 ms of load:
     # warm-up steps continue (untimed) until this much warm-up time has passed
     ap.add_argument("--min-warmup-s", type=float, default=0.5)
@@ -385,6 +441,8 @@ def main():
         }
         if world == 1:
             out["feed_frame_latency"] = feed_frame_latency(dev)
+            if not args.no_secondary:
+                out["secondary_configs"] = secondary_configs(dev)
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(layers)
             out["cpu_baseline_all_cores"] = cpu_baseline_all(tuple(topo))
