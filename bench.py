@@ -279,6 +279,9 @@ def main():
     ap.add_argument("--ffn", default="bl13", choices=["bl13", "ref39"])
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")  # skip the C2 / C5 lines (profiling runs)
+    # gloo: rehearse the N > 1 path on fewer GPUs than ranks (ranks share
+    # devices round-robin; the labels travel through host memory)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     # a GPU that was idle starts at low clocks and ramps for ~30 ms of load:
     # warm-up steps continue (untimed) until this much warm-up time has passed
     ap.add_argument("--min-warmup-s", type=float, default=0.5)
@@ -287,10 +290,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = local % torch.cuda.device_count() if args.backend == "gloo" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            dist.init_process_group("gloo")
 
     from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers
     from vad_amd.pipeline import VadPipeline

@@ -600,15 +600,27 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     LaneConsts L;
     lane_consts(plan, j, L);
     const int64_t flast = n_frames - 1;
+    // frame-granular, balanced runs: workgroup b owns frames
+    // [b F / G, (b + 1) F / G) in 64-frame tiles of its own; in a last,
+    // partial tile the waves whose frames all lie past the run skip phase 1
+    // (a tile-granular split leaves F / 64 mod G workgroups one full extra
+    // tile: a 7-tile makespan for 6.1 tiles of work at 100k frames)
+#ifndef VAD_FRAME_RUNS
+#define VAD_FRAME_RUNS 0  // 1: frame-granular runs (A/B: C2 -1.6 %, C3 +0.7 %)
+#endif
+    const int64_t f_beg = VAD_FRAME_RUNS ? n_frames * blockIdx.x / gridDim.x
+                                         : (int64_t)blockIdx.x * n_tiles / gridDim.x * kTile;
+    const int64_t f_end0 = VAD_FRAME_RUNS ? n_frames * (blockIdx.x + 1) / gridDim.x
+                                          : ((int64_t)blockIdx.x + 1) * n_tiles / gridDim.x * kTile;
+    const int64_t f_end = f_end0 < n_frames ? f_end0 : n_frames;
     auto pair_base = [&](int64_t t, int& lim) {
       if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
-      const int64_t F = t * kTile + 2 * grp;
+      const int64_t F = f_beg + t * kTile + 2 * grp;
       lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
       return src + (F < flast ? F : flast) * frame_stride;
     };
-    // contiguous, balanced runs: workgroup b owns tiles [b T / G, (b + 1) T / G)
-    int64_t tile = (int64_t)blockIdx.x * n_tiles / gridDim.x;
-    const int64_t t_end = ((int64_t)blockIdx.x + 1) * n_tiles / gridDim.x;
+    int64_t tile = 0;  // local tile index
+    const int64_t t_end = (f_end - f_beg + kTile - 1) / kTile;
     v2f buf[NB];
     {
       int lim;
@@ -634,54 +646,57 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     auto tile_body = [&](v2f (&buf)[NB]) {
       unsigned long long st_[kStamps];
       (void)st_;
-      const int64_t f0 = tile * kTile;
+      const int64_t f0 = f_beg + tile * kTile;
       const int64_t fa = f0 + 2 * grp, fb = fa + 1;
+      const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
       float* prow_a;
       float* prow_b;
       if constexpr (MODE == kAudioToSpec) {
-        prow_a = out + (fa < n_frames ? fa : flast) * kBins;
-        prow_b = out + (fb < n_frames ? fb : flast) * kBins;
+        prow_a = out + (fa < f_end ? fa : flast) * kBins;
+        prow_b = out + (fb < f_end ? fb : flast) * kBins;
       } else {
         prow_a = P + (2 * grp) * kPStride;
         prow_b = P + (2 * grp + 1) * kPStride;
       }
       int lim;
       const TIN* nb = pair_base(tile + 1, lim);
-      v2f u[16], col[32];
-      VAD_STAMP(0);
-      VAD_MILESTONE(3);
-      stage_a_at<NZ, LEN, 0>(buf, L, j, u);
-      VAD_STAMP(1);
-      __builtin_amdgcn_sched_barrier(0);
-      load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
-      __builtin_amdgcn_sched_barrier(0);
-      store_a(u, gscr, j);
-      read_b(L, gscr, col);
-      __builtin_amdgcn_sched_barrier(0);
-      VAD_STAMP(2);
-      VAD_MILESTONE(2);
-      // pass 1's stage A covers the latency of pass 0's transpose reads
-      stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
-      __builtin_amdgcn_sched_barrier(0);
-      load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
-      __builtin_amdgcn_sched_barrier(0);
-      VAD_STAMP(3);
-      VAD_MILESTONE(1);
-      if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
-      __builtin_amdgcn_sched_barrier(0);
-      load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
-      __builtin_amdgcn_sched_barrier(0);
-      VAD_STAMP(4);
-      VAD_MILESTONE(0);
-      store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
-      read_b(L, gscr, col);
-      VAD_STAMP(5);
-      if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+      if (active) {  // phase 1
+        v2f u[16], col[32];
+        VAD_STAMP(0);
+        VAD_MILESTONE(3);
+        stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+        VAD_STAMP(1);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
+        __builtin_amdgcn_sched_barrier(0);
+        VAD_STAMP(2);
+        VAD_MILESTONE(2);
+        // pass 1's stage A covers the latency of pass 0's transpose reads
+        stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        VAD_STAMP(3);
+        VAD_MILESTONE(1);
+        if (MODE != kAudioToSpec || fa < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+        __builtin_amdgcn_sched_barrier(0);
+        load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+        __builtin_amdgcn_sched_barrier(0);
+        VAD_STAMP(4);
+        VAD_MILESTONE(0);
+        store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
+        read_b(L, gscr, col);
+        VAD_STAMP(5);
+        if (MODE != kAudioToSpec || fb < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+      }
       if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(6);
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, f_end, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -703,7 +718,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
 
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, f_end, mfcc_n, out);
     }
     if constexpr (DIAG == 9) {
       __syncthreads();

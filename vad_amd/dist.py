@@ -124,13 +124,20 @@ class LabelGather:
         self.dst, self.global_dst = _group_dst(dst, group)
         self.rank = dist.get_rank(group)  # rank within the group, as dst
         world = dist.get_world_size(group)
-        self.out = [torch.empty((self.n,), dtype=torch.uint8, device=device) for _ in range(world)]
-        self.use_gather = str(dist.get_backend(group)).lower() in self.GATHER_BACKENDS
+        backend = str(dist.get_backend(group)).lower()
+        self.use_gather = backend in self.GATHER_BACKENDS
+        # gloo collectives take host tensors: device labels are staged through
+        # host memory (the CPU tests and the N > 1 rehearsal on one GPU)
+        self.via_host = backend == "gloo" and torch.device(device).type == "cuda"
+        bdev = "cpu" if self.via_host else device
+        self.out = [torch.empty((self.n,), dtype=torch.uint8, device=bdev) for _ in range(world)]
 
     def __call__(self, labels: torch.Tensor):
         if labels.numel() != self.n or labels.dtype != torch.uint8:
             raise ValueError(f"expected {self.n} uint8 labels, got {labels.numel()} {labels.dtype}")
         x = labels.reshape(-1)
+        if self.via_host:
+            x = x.cpu()
         if self.use_gather:
             dist.gather(x, self.out if self.rank == self.dst else None, dst=self.global_dst,
                         group=self.group)
