@@ -346,7 +346,10 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
     net.boff[l] = (int)wraw.size();
     wraw.insert(wraw.end(), b[l], b[l] + dims[l + 1]);
   }
-  while (wraw.size() % 4) wraw.push_back(0.f);  // whole 16-B vectors for the LDS staging
+  // zero rows past the last layer (the streaming forward reads its inputs in
+  // fours: up to three weight rows past W_l), whole 16-B vectors
+  wraw.insert(wraw.end(), 3 * 64 + 4, 0.f);
+  while (wraw.size() % 4) wraw.push_back(0.f);
   net.wraw_n = (int)wraw.size();
 
   vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));

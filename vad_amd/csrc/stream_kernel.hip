@@ -117,7 +117,16 @@ hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t 
 #ifndef VAD_HOP_DIAG
 #define VAD_HOP_DIAG 0  // diagnostic builds only: stop after 1 staging, 2 FFT, 3 mel / DCT, 4 features
 #endif
-constexpr int kHopZ = 2 * 256;                     // one 256-point complex buffer
+#ifndef VAD_HOP_Q
+#define VAD_HOP_Q 4
+#endif
+constexpr int kHopZ = 2 * (256 + 32);              // one 256-point complex buffer, padded
+// complex element i of a buffer sits at i + i / 8: the Stockham stores of the
+// first stages (stride 4 and 16 complex across lanes) spread over the banks
+#ifndef VAD_HOP_PAD
+#define VAD_HOP_PAD 1
+#endif
+__device__ __forceinline__ int zp(int i) { return VAD_HOP_PAD ? i + (i >> 3) : i; }
 constexpr int kHopWaveFloats = 2 * kHopZ + kMaxFilters + 64 + 64;
 
 // Block-shared LDS, staged once per block from the plans (the per-stream
@@ -161,15 +170,16 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     const float4* w4 = reinterpret_cast<const float4*>(net.wraw);
     float4* d4 = reinterpret_cast<float4*>(base);
     const int nm4 = blob_n >> 2, n4 = nm4 + (net.wraw_n >> 2);
-    for (int i0 = 0; i0 < n4; i0 += 4 * (int)blockDim.x) {
-      float4 t[4];
+    constexpr int kQ = VAD_HOP_Q;  // 16-B loads in flight per thread
+    for (int i0 = 0; i0 < n4; i0 += kQ * (int)blockDim.x) {
+      float4 t[kQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < kQ; ++q) {
         const int i = i0 + q * blockDim.x + threadIdx.x;
         t[q] = i < nm4 ? m4[i] : (i < n4 ? w4[i - nm4] : make_float4(0.f, 0.f, 0.f, 0.f));
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < kQ; ++q) {
         const int i = i0 + q * blockDim.x + threadIdx.x;
         if (i < n4) d4[i] = t[q];
       }
@@ -229,8 +239,8 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   float* xs = reinterpret_cast<float*>(z1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    const int t = lane + 64 * i;
-    xs[t] = t < used ? v[i] : 0.f;
+    const int t = lane + 64 * i;  // sample t = component t & 1 of complex t / 2
+    xs[2 * zp(t >> 1) + (t & 1)] = t < used ? v[i] : 0.f;
   }
   // LDS is in order within a wave; these keep the compiler from moving
   // accesses of one phase (other lanes' data, other element types) across
@@ -244,7 +254,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   for (int st = 0; st < 4; ++st) {
     const int ns = 1 << (2 * st);  // 1, 4, 16, 64
     const int k = lane & (ns - 1);
-    float2 a0 = src[lane], a1 = src[lane + 64], a2 = src[lane + 128], a3 = src[lane + 192];
+    float2 a0 = src[zp(lane)], a1 = src[zp(lane + 64)], a2 = src[zp(lane + 128)], a3 = src[zp(lane + 192)];
     if (st > 0) {
       const int m = k * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
       a1 = cmulf(a1, w256(T.tw, m));
@@ -254,10 +264,10 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
     const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
     const int o = (lane >> (2 * st)) * (4 * ns) + k;
-    dst[o] = make_float2(b0.x + b2.x, b0.y + b2.y);
-    dst[o + ns] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
-    dst[o + 2 * ns] = make_float2(b0.x - b2.x, b0.y - b2.y);
-    dst[o + 3 * ns] = make_float2(b1.x - b3.y, b1.y + b3.x);  // b1 + i b3
+    dst[zp(o)] = make_float2(b0.x + b2.x, b0.y + b2.y);
+    dst[zp(o + ns)] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
+    dst[zp(o + 2 * ns)] = make_float2(b0.x - b2.x, b0.y - b2.y);
+    dst[zp(o + 3 * ns)] = make_float2(b1.x - b3.y, b1.y + b3.x);  // b1 + i b3
     float2* t = src;
     src = dst;
     dst = t;
@@ -274,7 +284,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int k = lane + 64 * q;
-    const float2 zk = src[k], zn = src[(256 - k) & 255];
+    const float2 zk = src[zp(k)], zn = src[zp((256 - k) & 255)];
     const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
     const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
     const float2 Tw = cmulf(D, T.tw[k]);
@@ -309,6 +319,8 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   }
   // -- window of the five previous frames, then push the new row
   const bool have = c >= 5;
+  act_a[lane] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
+  asm volatile("" ::: "memory");
   if (lane < mfcc_n) {
     if (have) {
       // slot (c + d) % 5, d = 0..4: the ring in arrival order, oldest first
@@ -334,13 +346,32 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     const int nl = net.n_layers;
     for (int l = 0; l < nl; ++l) {
       const int din = net.dims[l], dout = net.dims[l + 1];
+#ifndef VAD_HOP_VEC
+#define VAD_HOP_VEC 1
+#endif
+      // four inputs per step (one ds_read_b128 broadcast), four partial
+      // sums; inputs past din are zero and the weight rows past W_l read
+      // the next finite values of the block (zero-padded at its end)
+      const float* W = T.w + net.woff[l];
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
       if (lane < dout) {
-        const float* W = T.w + net.woff[l];
-        float acc = T.w[net.boff[l] + lane];
+        if (VAD_HOP_VEC) {
+          const float4* h4 = reinterpret_cast<const float4*>(hin);
+#pragma unroll 4
+          for (int k = 0; k < din; k += 4) {
+            const float4 h = h4[k >> 2];
+            a0 = fmaf(W[k * dout + lane], h.x, a0);
+            a1 = fmaf(W[(k + 1) * dout + lane], h.y, a1);
+            a2 = fmaf(W[(k + 2) * dout + lane], h.z, a2);
+            a3 = fmaf(W[(k + 3) * dout + lane], h.w, a3);
+          }
+        } else {
 #pragma unroll 8
-        for (int k = 0; k < din; ++k) acc = fmaf(W[k * dout + lane], hin[k], acc);
-        hout[lane] = l + 1 < nl ? relu_nan(acc) : acc;
+          for (int k = 0; k < din; ++k) a0 = fmaf(W[k * dout + lane], hin[k], a0);
+        }
       }
+      const float acc = T.w[net.boff[l] + (lane < dout ? lane : 0)] + ((a0 + a1) + (a2 + a3));
+      hout[lane] = lane < dout ? (l + 1 < nl ? relu_nan(acc) : acc) : 0.f;
       float* t = hin;
       hin = hout;
       hout = t;
