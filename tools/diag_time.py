@@ -1,4 +1,5 @@
-"""Time mfcc_kernel (1M frames) for the VAD_DIAG ablation set in the env."""
+"""Time mfcc_kernel (1M frames) of the library VAD_AMD_LIB names (A/B of
+variant builds: python -m vad_amd.build --variant NAME -D...)."""
 import os
 import sys
 

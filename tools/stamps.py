@@ -1,4 +1,4 @@
-"""Phase timing of mfcc_kernel from in-kernel s_memtime stamps (VAD_DIAG=5)."""
+"""Phase timing of mfcc_kernel from in-kernel s_memtime stamps (a -DVAD_DIAG_BUILD=5 library)."""
 import os
 import sys
 
@@ -6,7 +6,11 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("VAD_DIAG", "5")
+# the stamps come from a diagnostic library build (the shipped one has none):
+#   python -m vad_amd.build --variant diag5 -DVAD_DIAG_BUILD=5
+os.environ.setdefault("VAD_AMD_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "vad_amd", "lib", "libvad_amd_diag5.so"))
+os.environ.setdefault("VAD_DIAG", "5")  # read by this script only
 from bench import synth_audio  # noqa: E402
 from vad_amd.pipeline import VadPipeline  # noqa: E402
 

@@ -1,4 +1,4 @@
-"""Per-workgroup start/end stamps of mfcc_kernel (VAD_DIAG=9): shader clock,
+"""Per-workgroup start/end stamps of mfcc_kernel (a -DVAD_DIAG_BUILD=9 library): shader clock,
 workgroup durations vs kernel wall time, dispatch skew."""
 import os
 import sys
@@ -7,7 +7,11 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("VAD_DIAG", "9")
+# the stamps come from a diagnostic library build (the shipped one has none):
+#   python -m vad_amd.build --variant diag9 -DVAD_DIAG_BUILD=9
+os.environ.setdefault("VAD_AMD_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "vad_amd", "lib", "libvad_amd_diag9.so"))
+os.environ.setdefault("VAD_DIAG", "9")  # read by this script only
 from bench import synth_audio  # noqa: E402
 from vad_amd.pipeline import VadPipeline  # noqa: E402
 
