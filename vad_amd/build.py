@@ -77,6 +77,19 @@ def build(force=False, verbose=True, defines=(), out=None):
     return lib
 
 
+C_HOST_DIR = os.path.join(os.path.dirname(HERE), "tests", "c_host")
+
+
+def build_c_host(verbose=True):
+    """The plain-C test host (tests/c_host): gcc against include/vad_amd.h and
+    the in-tree library, built here so GPU runs only execute it."""
+    cmd = ["make", "-C", C_HOST_DIR, "-s", "capi_host"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return os.path.join(C_HOST_DIR, "capi_host")
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
     if "--variant" in args:  # python -m vad_amd.build --variant NAME -DX=1 ...
