@@ -273,17 +273,33 @@ __device__ __forceinline__ float wave_max(float v) {
 // f16 (NaN passes through f16 as NaN and does not count), else the power of
 // two that brings the wave's largest into [2^14, 2^15) -- the inputs are
 // scaled in place and the layer unscales its result exactly.
-template <int K>
+template <int K, bool NONNEG = false>
 __device__ __forceinline__ float layer_scale(float (&v)[K][8]) {
   // inputs are NaN-free (ffn_window_body masks NaN windows) and VALU
   // results or LDS reads (never MFMA results, whose read hazard inline asm
-  // would hide): one v_max3 per pair, no canonicalising maxNum sequence
+  // would hide): one v_max3 per pair, no canonicalising maxNum sequence.
+  // NONNEG (the ReLU'd inputs of layers >= 1): an unsigned-integer max3 on
+  // the bits, which orders non-negative floats like their values (no asm,
+  // so no hazard padding around it)
   float m = 0.f;
+  if constexpr (NONNEG) {
+    unsigned mb = 0u;
 #pragma unroll
-  for (int s = 0; s < K; ++s)
+    for (int s = 0; s < K; ++s)
 #pragma unroll
-    for (int q = 0; q < 8; q += 2)
-      asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[s][q]), "v"(v[s][q + 1]));
+      for (int q = 0; q < 8; ++q) {
+        const float e = v[s][q];
+        const unsigned b = __builtin_bit_cast(unsigned, e);
+        mb = mb > b ? mb : b;
+      }
+    m = __builtin_bit_cast(float, mb);
+  } else {
+#pragma unroll
+    for (int s = 0; s < K; ++s)
+#pragma unroll
+      for (int q = 0; q < 8; q += 2)
+        asm("v_max3_f32 %0, %1, |%2|, |%3|" : "=v"(m) : "v"(m), "v"(v[s][q]), "v"(v[s][q + 1]));
+  }
   if (__builtin_amdgcn_ballot_w64(m >= kH3Max) == 0) return 1.f;
   // wave-uniform from here (readfirstlane): the callers' sc == 1 tests
   // become scalar branches, not exec-masked regions
@@ -314,9 +330,9 @@ __device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1
 
 // out[mt] = bias + sum_s lo*hi + hi*lo + hi*hi (small terms first) on inputs
 // v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
-template <int TO, int KS, class FB, class FH>
+template <int TO, int KS, class FB, bool NONNEG = false, class FH>
 __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu) {
-  const float sc = layer_scale<KS>(v);
+  const float sc = layer_scale<KS, NONNEG>(v);
   h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
@@ -358,11 +374,19 @@ __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&
 #pragma unroll
   for (int mt = 0; mt < TO; ++mt) {
     f32x4 o = acc[mt];
-    // NaN-free here: clamp to [0, inf) is the ReLU (a builtin, not asm: the
-    // operand is an MFMA result, whose read hazard the compiler must see)
+    // NaN-free here, so the ReLU is a signed-integer max with 0 on the bits
+    // (negative floats, -0 included, are negative integers): one v_max_i32
+    // per value -- a float max / med3 on an MFMA result compiles to a
+    // canonicalising v_max_f32 first, two instructions per value
     if (relu) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = __builtin_amdgcn_fmed3f(o[r], 0.f, __builtin_inff());
+      for (int r = 0; r < 4; ++r) {
+        // (the element goes through a scalar first: clang's bit_cast of an
+        // ext_vector element expression reads element 0 whatever the index)
+        const float e = o[r];
+        const int bits = __builtin_bit_cast(int, e);
+        o[r] = __builtin_bit_cast(float, bits > 0 ? bits : 0);
+      }
     }
     out[mt] = o;
   }
@@ -422,14 +446,14 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)
     float v1[HP::K1][8];
     acts_of<T1>(h1, v1);
     f32x4 h2[T2];
-    dense_h3<T2, HP::K1, FB>(fh.at(HP::S0), fb + 4 * T1, v1, h2, TP::NL > 2);
+    dense_h3<T2, HP::K1, FB, true>(fh.at(HP::S0), fb + 4 * T1, v1, h2, TP::NL > 2);
     if constexpr (TP::NL == 2) return h2[0];
     else if constexpr (TP::NL == 3 && TP::VL) return valu_out_layer<TP, T2, FV>(fv, h2);
     else {
       float v2[HP::K2][8];
       acts_of<T2>(h2, v2);
       f32x4 h3[T3];
-      dense_h3<T3, HP::K2, FB>(fh.at(HP::S0 + HP::S1), fb + 4 * (T1 + T2), v2, h3,
+      dense_h3<T3, HP::K2, FB, true>(fh.at(HP::S0 + HP::S1), fb + 4 * (T1 + T2), v2, h3,
                                TP::NL > 3);
       if constexpr (TP::NL == 3) return h3[0];
       else if constexpr (TP::VL) return valu_out_layer<TP, T3, FV>(fv, h3);
@@ -437,7 +461,7 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)
         float v3[HP::K3][8];
         acts_of<T3>(h3, v3);
         f32x4 h4[T4];
-        dense_h3<T4, HP::K3, FB>(fh.at(HP::S0 + HP::S1 + HP::S2), fb + 4 * (T1 + T2 + T3),
+        dense_h3<T4, HP::K3, FB, true>(fh.at(HP::S0 + HP::S1 + HP::S2), fb + 4 * (T1 + T2 + T3),
                                  v3, h4, false);
         return h4[0];
       }
