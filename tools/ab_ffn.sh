@@ -1,6 +1,6 @@
 set -e
 for i in 1 2 3; do
-  for L in base ""; do
+  for L in s0 ""; do
     if [ -z "$L" ]; then export VAD_AMD_LIB=vad_amd/lib/libvad_amd.so; else export VAD_AMD_LIB=vad_amd/lib/libvad_amd_$L.so; fi
     echo "lib=$VAD_AMD_LIB"; timeout -k 10 120 python tools/diag_ffn.py
   done

@@ -33,6 +33,32 @@ __device__ void mfma_work(float* out, int iters) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = r;
 }
 
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+// the FFN's MFMA: v_mfma_f32_16x16x32_f16, 4 independent accumulators
+__device__ void mfma16_work(float* out, int iters) {
+  v4f acc[4] = {};
+  h8 a, b;
+  for (int i = 0; i < 8; ++i) { a[i] = (_Float16)(threadIdx.x * 0.001f); b[i] = (_Float16)1.f; }
+  for (int it = 0; it < iters; ++it)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, acc[i], 0, 0, 0);
+  float r = 0.f;
+  for (int i = 0; i < 4; ++i) r += acc[i].x + acc[i].y + acc[i].z + acc[i].w;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+// scalar fp32 VALU (the FFN's epilogues are mostly scalar)
+__device__ void svalu_work(float* out, int iters) {
+  float a[16];
+  const float m1 = 1.0001f;
+  for (int i = 0; i < 16; ++i) a[i] = (float)threadIdx.x * i;
+  for (int it = 0; it < iters; ++it)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) asm volatile("v_fma_f32 %0, %0, %1, 0.5" : "+v"(a[i]) : "v"(m1));
+  float r = 0.f;
+  for (int i = 0; i < 16; ++i) r += a[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = r;
+}
+
 __global__ void k(float* out, int mode, int iters_v, int iters_m) {
   const int w = threadIdx.x >> 6;
   const bool older = w < 4;
@@ -42,6 +68,10 @@ __global__ void k(float* out, int mode, int iters_v, int iters_m) {
   else if (mode == 3) { if (older) mfma_work(out, iters_m); }
   else if (mode == 4) { if (!older) valu_work(out, iters_v); }
   else if (mode == 5) { if (older) valu_work(out, iters_v); else mfma_work(out, iters_m); }
+  else if (mode == 6) { if (older) mfma16_work(out, iters_m); }
+  else if (mode == 7) { if (!older) svalu_work(out, iters_v); }
+  else if (mode == 8) { if (older) mfma16_work(out, iters_m); else svalu_work(out, iters_v); }
+  else if (mode == 9) { if (older) svalu_work(out, iters_v); else svalu_work(out, iters_v); }
 }
 
 int main() {
@@ -50,11 +80,13 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
-  const int iv = 4000;  // 64k pk_fma per wave
-  const int im = 2000;  // 8k MFMA per wave (x32 cyc = 256k cyc)
+  const int iv = 40000;  // 64k pk_fma per wave
+  const int im = 20000;  // 8k MFMA per wave (x32 cyc = 256k cyc)
   const char* names[] = {"both VALU", "both MFMA", "old MFMA + young VALU", "old MFMA only",
-                         "young VALU only", "old VALU + young MFMA"};
-  for (int mode = 0; mode < 6; ++mode) {
+                         "young VALU only", "old VALU + young MFMA", "old f16 MFMA only",
+                         "young scalar VALU only", "old f16 MFMA + young scalar", "both scalar VALU"};
+  for (int mm = 0; mm < 20; ++mm) {
+    const int mode = mm % 10;
     float best = 1e30f;
     for (int rep = 0; rep < 4; ++rep) {
       (void)hipEventRecord(e0);

@@ -317,10 +317,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 // the 128-VGPR budget spills: 140 us).  With more than two classes its
 // output layer no longer fits beside the VGPR fragments (scratch spills:
 // 101 us for 13-64-64-3), so those read the fragments from LDS too (78 us).
+#ifndef VAD_FFN_LDS_SLOTS
+#define VAD_FFN_LDS_SLOTS 1
+#endif
+// kLdsSlots (13-64-64-2): the bias and VALU output-layer slots (one value
+// per lane group) move to a workgroup-shared LDS table read per tile, which
+// frees their ~70 VGPRs for a third wave per SIMD while the split-f16
+// fragments stay in VGPRs (a lone wave issues scalar VALU work at about a
+// third of the rate two waves reach together: tools/micro/mfma_valu_overlap)
 template <int KS0, int NC>
 struct WaveResidency {
   static constexpr bool kLdsFrags = KS0 == 10 || NC > 2;
-  static constexpr int kWavesPerSimd = KS0 == 10 ? 3 : 2;
+  static constexpr bool kLdsSlots = VAD_FFN_LDS_SLOTS != 0 && !kLdsFrags;
+  static constexpr int kWavesPerSimd = KS0 == 10 ? 3 : kLdsSlots ? 3 : 2;
+};
+// Fragments with the hi halves (and layer 0's lo halves) in VGPRs and the lo
+// halves of slots >= LO_FROM read from a workgroup-shared LDS copy
+// ([slot - LO_FROM][lane], one ds_read_b128 per MFMA that uses one): the
+// register file keeps the operands of two of the three products per layer.
+template <int LO_FROM>
+struct FragSplitRes {
+  const u4 (*p)[2];
+  const u4* lo;  // fhlo_s + lane
+  int base;      // slot offset of this accessor (compile-time after inlining)
+  __device__ u4 get(int sl, int h) const {
+    return (h == 1 && base + sl >= LO_FROM) ? lo[(base + sl - LO_FROM) * 64] : p[sl][h];
+  }
+  __device__ FragSplitRes at(int off) const { return {p + off, lo, base + off}; }
+};
+// a lane group's row of the slot table: slot s at p[s] (16-B aligned rows,
+// so a layer's four consecutive bias slots are one ds_read_b128)
+struct LdsRow {
+  const float* p;
+  __device__ float operator[](int s) const { return p[s]; }
+  __device__ LdsRow operator+(int off) const { return {p + off}; }
 };
 constexpr int kWRows = (kWTile + 4) * 13;        // staged MFCC floats per tile (260)
 constexpr int kWRowRegs = (kWRows + 63) / 64;    // 5 per lane
@@ -348,11 +378,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
   float* X = x_s[wv];
   int* FL = flat_s[wv];
 
-  float fa[1];
-  float fb[TP::NB];
-  float fv[TP::NV + TP::NVB + 1];
-  load_frags<TP, true>(net.frag, lane, fa, fb, fv);
   constexpr bool kLdsFrags = WaveResidency<KS0, NC>::kLdsFrags;
+  constexpr bool kLdsSlots = WaveResidency<KS0, NC>::kLdsSlots;
+  constexpr int NSL = TP::NB + TP::NV + TP::NVB;  // bias + output-layer slots
+  constexpr int NSLP = (NSL + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float slot_s[kLdsSlots ? 4 * NSLP : 1];
+#ifndef VAD_FFN_LO_ALL
+#define VAD_FFN_LO_ALL 1  // 1: every lo half in LDS; 0: those after layer 0 only
+#endif
+  constexpr int kLoFrom = VAD_FFN_LO_ALL ? 0 : HP::S0;
+  constexpr int kLoSlots = kLdsSlots ? HP::NS - kLoFrom : 0;
+  __shared__ u4 fhlo_s[kLoSlots > 0 ? kLoSlots * 64 : 1];
+  float fa[1];
+  float fb[kLdsSlots ? 1 : TP::NB];
+  float fv[kLdsSlots ? 1 : TP::NV + TP::NVB + 1];
+  if constexpr (kLdsSlots) {
+    // slot sl of lane group gg (the host's fragment order: biases, then the
+    // VALU layer's class slots, then its biases after 4 classes' worth)
+    for (int i = threadIdx.x; i < 4 * NSLP; i += 256) {
+      const int gg = i / NSLP, sl = i - gg * NSLP;
+      const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
+                                     : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
+                                                                                  : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
+      slot_s[i] = sl < NSL ? net.frag[src_sl * 64 + 16 * gg] : 0.f;
+    }
+    // the lo halves of the layers after the first: [slot - S0][lane]
+    for (int i = threadIdx.x; i < kLoSlots * 64; i += 256)
+      fhlo_s[i] = reinterpret_cast<const u4*>(net.fragh)[(2 * (kLoFrom + i / 64) + 1) * 64 + (i & 63)];
+    __syncthreads();
+  } else {
+    load_frags<TP, true>(net.frag, lane, fa, fb, fv);
+  }
+  const auto fbs = [&] {
+    if constexpr (kLdsSlots) return LdsRow{slot_s + g * NSLP};
+    else return (const float*)fb;
+  }();
+  const auto fvs = [&] {
+    if constexpr (kLdsSlots) return LdsRow{slot_s + g * NSLP + TP::NB};
+    else return (const float*)fv;
+  }();
   __shared__ u4 fh_s[kLdsFrags ? HP::NS * 2 * 64 : 1];
   u4 fh_r[kLdsFrags ? 1 : HP::NS][2];
   if constexpr (kLdsFrags) {
@@ -363,6 +427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
   }
   const auto fh = [&] {
     if constexpr (kLdsFrags) return FragLds{fh_s, lane};
+    else if constexpr (kLdsSlots) return FragSplitRes<kLoFrom>{fh_r, fhlo_s + lane, 0};
     else return FragRegs{fh_r};
   }();
   // feature columns IN .. 32 K0 - 1 are read by layer 0 and stay 0
@@ -401,7 +466,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
     f32x4 z;
     const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false>(
-        X, FL, lane, fh, (const float*)fb, (const float*)fv, net.n_classes, z);
+        X, FL, lane, fh, fbs, fvs, net.n_classes, z);
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) {
       labels[w] = (uint8_t)lab;
