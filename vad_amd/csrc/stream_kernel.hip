@@ -394,10 +394,12 @@ hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n,
   (void)plan;
   if (n_streams <= 0) return hipSuccess;
   const size_t tables = (size_t)(blob_n + net.wraw_n) * sizeof(float);
-  // streams per block: spread over every CU first (each block stages the
-  // ~26 KB of tables from L2 once; the per-stream chain is LDS-bound, so
-  // fewer waves per CU run it faster), up to 16 waves when there are more
-  // streams than CUs, and as many as the LDS holds
+  // streams per block: at least VAD_HOP_MIN_WAVES (one wave per SIMD), then
+  // spread over every CU (each block stages the ~26 KB of tables from L2
+  // once; the per-stream chain is LDS-bound, so fewer waves per CU run it
+  // faster), up to 16 waves when there are more streams than CUs, and as
+  // many as the LDS holds.  512 streams, A/B on one box: 2 waves per block
+  // on 256 CUs 11.0-11.3 us per hop, 4 on 128 CUs 10.4, 8 on 64 CUs 10.8
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -405,7 +407,10 @@ hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n,
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
       n_cu = 256;
   }
-  int waves = 1;
+#ifndef VAD_HOP_MIN_WAVES
+#define VAD_HOP_MIN_WAVES 4
+#endif
+  int waves = VAD_HOP_MIN_WAVES;
   while (waves < 16 && (int64_t)waves * n_cu < n_streams) waves <<= 1;
   while (waves > 1 && tables + (size_t)waves * kHopWaveFloats * sizeof(float) > 160 * 1024) waves >>= 1;
   const size_t smem = tables + (size_t)waves * kHopWaveFloats * sizeof(float);
