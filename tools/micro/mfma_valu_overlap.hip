@@ -76,7 +76,7 @@ __global__ void k(float* out, int mode, int iters_v, int iters_m) {
 
 int main() {
   float* out;
-  (void)hipMalloc(&out, 256 * 512 * 4);
+  (void)hipMalloc(&out, 256 * 1024 * 4);
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -98,6 +98,25 @@ int main() {
       if (rep > 0 && ms < best) best = ms;
     }
     printf("%-24s %.3f ms\n", names[mode], best);
+  }
+  // waves per SIMD 1 / 2 / 3 / 4 (blocks of 256 / 512 / 768 / 1024 threads,
+  // every wave busy): scalar (mode 9) and packed (mode 0) throughput per SIMD
+  for (int wps = 1; wps <= 4; ++wps) {
+    for (int mode : {9, 0}) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 4; ++rep) {
+        (void)hipEventRecord(e0);
+        k<<<256, 256 * wps>>>(out, mode, iv, im);
+        (void)hipEventRecord(e1);
+        (void)hipDeviceSynchronize();
+        float ms;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (rep > 0 && ms < best) best = ms;
+      }
+      // instructions per SIMD: wps waves x iv x 16
+      printf("%d waves/SIMD %-7s %.3f ms  %.3f ns per wave-instruction per SIMD\n", wps,
+             mode == 9 ? "scalar" : "packed", best, best * 1e6 / (wps * (double)iv * 16));
+    }
   }
   return 0;
 }
