@@ -1,6 +1,6 @@
 """A/B of MFCC kernel builds on one box: python tools/ab_mfcc.py LIB_A LIB_B [rounds]
 Alternates the two libraries (fresh processes) and prints per-launch us for
-C3 (1M frames) and C2 (100k, 6 rotated clips), fp32 input."""
+C3 (1M frames) and C2 (100k, 6 rotated clips), fp32 input (int16 PCM with AB_I16=1)."""
 import json
 import os
 import subprocess
@@ -22,10 +22,12 @@ def t(fn, reps=100, warm=200):
     return s.elapsed_time(e) / reps * 1e3
 F = 1_000_000
 a = synth_audio(160 * (F - 1) + 401, 1, dev); m = torch.empty((F, 13), device=dev)
+if os.environ.get("AB_I16"): a = a.to(torch.int16)
 c3 = t(lambda: pipe.mfcc(a, out=m))
 del a, m
 F = 100_000
 cl = [synth_audio(160 * (F - 1) + 401, 10 + i, dev) for i in range(6)]; m = torch.empty((F, 13), device=dev)
+if os.environ.get("AB_I16"): cl = [c.to(torch.int16) for c in cl]
 k = [0]
 def c2f():
     pipe.mfcc(cl[k[0] % 6], out=m); k[0] += 1

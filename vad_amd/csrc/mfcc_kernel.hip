@@ -74,6 +74,9 @@ struct Samples<float> {
 #endif
   }
   __device__ static float one(const float* p) { return *p; }
+  __device__ static v2f raw_pair(const float* p) { return pair(p); }
+  __device__ static v2f raw_two(const float* p0, const float* p1) { return (v2f){*p0, *p1}; }
+  __device__ static v2f cvt(v2f r) { return r; }
 };
 template <>
 struct Samples<int16_t> {
@@ -87,6 +90,26 @@ struct Samples<int16_t> {
     return (v2f){(float)(int16_t)(v & 0xffff), (float)(v >> 16)};
   }
   __device__ static float one(const int16_t* p) { return (float)*p; }
+  // prefetched pairs stay raw (the two int16 in one dword, in .x) until
+  // their stage A: converting at the load would wait for it right there
+  // (the loads sit in sched_barrier-fenced regions), which serialised the
+  // one-tile-ahead prefetch of the int16 kernel
+  __device__ static v2f raw_pair(const int16_t* p) {
+#if VAD_NT_LOADS
+    const int v = __builtin_nontemporal_load(reinterpret_cast<const int*>(p));
+#else
+    const int v = *reinterpret_cast<const int*>(p);
+#endif
+    return (v2f){__builtin_bit_cast(float, v), 0.f};
+  }
+  __device__ static v2f raw_two(const int16_t* p0, const int16_t* p1) {
+    const int v = (int)(unsigned short)*p0 | ((int)*p1 << 16);
+    return (v2f){__builtin_bit_cast(float, v), 0.f};
+  }
+  __device__ static v2f cvt(v2f r) {
+    const int v = __builtin_bit_cast(int, r.x);
+    return (v2f){(float)(int16_t)(v & 0xffff), (float)(v >> 16)};
+  }
 };
 
 // Load z[16 n1 + n2] = (x[32 n1 + 2 n2], x[32 n1 + 2 n2 + 1]), n1 < NZ.
@@ -114,11 +137,11 @@ __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len
     const int t = 32 * n1 + 2 * n2;
     if constexpr (VEC2) {
       const int tc = t < len - 2 ? t : len - 2;
-      u[n1] = Samples<TIN>::pair(fr + tc);
+      u[n1] = Samples<TIN>::raw_pair(fr + tc);
     } else {
       const int t0 = t < len - 1 ? t : len - 1;
       const int t1 = t + 1 < len - 1 ? t + 1 : len - 1;
-      u[n1] = (v2f){Samples<TIN>::one(fr + t0), Samples<TIN>::one(fr + t1)};
+      u[n1] = Samples<TIN>::raw_two(fr + t0, fr + t1);
     }
   }
 }
@@ -239,12 +262,15 @@ __device__ __forceinline__ void lane_consts_lds(const v2f* __restrict__ tw, int 
 // SCALE multiplies |2X|^2 into P = |X/512|^2 (2^-20); the MFCC modes fold
 // that factor into the mel taps.  Every complex operation is packed fp32
 // (fft_pk.h).
-template <int NZ, int LEN>
-__device__ __forceinline__ void stage_a(v2f (&u_in)[NZ], int len, const LaneConsts& L, int j,
-                                        v2f (&u)[16]) {
-  pad_stage_a<NZ, LEN>(len, j, u_in);
+template <typename TIN, int NZ, int LEN, bool WIN = false>
+__device__ __forceinline__ void stage_a(const v2f (&u_in)[NZ], int len, const LaneConsts& L, int j,
+                                        v2f (&u)[16], const float* wv = nullptr) {
 #pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = u_in[n];
+  for (int n = 0; n < NZ; ++n) {
+    u[n] = Samples<TIN>::cvt(u_in[n]);
+    if constexpr (WIN) u[n] = u[n] * (v2f){wv[2 * n], wv[2 * n + 1]};
+  }
+  pad_stage_a<NZ, LEN, 16>(len, j, u);
   pk::dft16<NZ>(u);
 #pragma unroll
   for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
@@ -264,16 +290,16 @@ __device__ __forceinline__ void load_chunks(const TIN* __restrict__ base, int li
   for (int c = B; c < E; ++c) {
     int o = 32 * c + 2 * n2;
     if (32 * c + 30 > LEN - 2) o = o < lim ? o : lim;
-    buf[c] = Samples<TIN>::pair(base + o);
+    buf[c] = Samples<TIN>::raw_pair(base + o);
   }
 }
 
 // stage A of the frame whose chunk n1 is buf[OFF + n1]
-template <int NZ, int LEN, int OFF, int NB>
+template <typename TIN, int NZ, int LEN, int OFF, int NB>
 __device__ __forceinline__ void stage_a_at(const v2f (&buf)[NB], const LaneConsts& L, int j,
                                            v2f (&u)[16]) {
 #pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = buf[OFF + n];
+  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[OFF + n]);
   pad_stage_a<NZ, LEN, 16>(LEN, j, u);
   pk::dft16<NZ>(u);
 #pragma unroll
@@ -513,10 +539,14 @@ constexpr int kStamps = 11;
 // (tile start, pass-0 transpose issued, pass-1 stage A, pass-0 power row),
 // so the younger wave of a SIMD, which loses every tie on age, gets the VALU
 // until it reaches the same milestone and the two reach the first barrier
-// closer together: -7 us per 1M frames on fp32 input, +3.5 us on int16
-// (left off there).
+// closer together: -7 us per 1M frames on fp32 input; on int16 input -4 us
+// since its samples are converted at first use (before that, with the
+// prefetch serialised by the conversion, +3.5 us).
+#ifndef VAD_PRIO_I16
+#define VAD_PRIO_I16 1
+#endif
 template <typename TIN>
-constexpr bool kMilestonePrio = std::is_same_v<TIN, float>;
+constexpr bool kMilestonePrio = std::is_same_v<TIN, float> || VAD_PRIO_I16;
 
 // (Placements measured: 3/2/1/0 at these four; 3/2/-/1 + 0 after the pass-1
 // power row +4 us; 3/-/2/1 + 0 there the same.  Spreading the DCT over all
@@ -664,7 +694,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         v2f u[16], col[32];
         VAD_STAMP(0);
         VAD_MILESTONE(3);
-        stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+        stage_a_at<TIN, NZ, LEN, 0>(buf, L, j, u);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
         load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
@@ -675,7 +705,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         VAD_STAMP(2);
         VAD_MILESTONE(2);
         // pass 1's stage A covers the latency of pass 0's transpose reads
-        stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
+        stage_a_at<TIN, NZ, LEN, HOPC>(buf, L, j, u);
         __builtin_amdgcn_sched_barrier(0);
         load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
@@ -741,12 +771,6 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         wv[2 * n1 + 1] = plan->window[32 * n1 + 2 * j + 1];
       }
     }
-    auto windowed = [&](v2f (&b)[NZ]) __attribute__((always_inline)) {
-      if constexpr (WIN) {
-#pragma unroll
-        for (int n1 = 0; n1 < NZ; ++n1) b[n1] = b[n1] * (v2f){wv[2 * n1], wv[2 * n1 + 1]};
-      }
-    };
     // software pipeline: the samples of the next pass are in flight while
     // the current pass computes
     v2f bufA[NZ], bufB[NZ];
@@ -805,7 +829,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // the texture address queue and hold every wave at its load burst
         const TIN* sa = pass_src(tile + 1, 0);
         const TIN* sb = pass_src(tile + 1, 1);
-        stage_a<NZ, LEN>(bufA, len, L, j, u);
+        stage_a<TIN, NZ, LEN>(bufA, len, L, j, u);
         __builtin_amdgcn_sched_barrier(0);
         load_stage_a<TIN, NZ, VEC2, LEN, 0, 5>(sa, len, j, bufA);
         __builtin_amdgcn_sched_barrier(0);
@@ -814,7 +838,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         __builtin_amdgcn_sched_barrier(0);
         load_stage_a<TIN, NZ, VEC2, LEN, 5, 9>(sa, len, j, bufA);
         __builtin_amdgcn_sched_barrier(0);
-        stage_a<NZ, LEN>(bufB, len, L, j, u);
+        stage_a<TIN, NZ, LEN>(bufB, len, L, j, u);
         __builtin_amdgcn_sched_barrier(0);
         load_stage_a<TIN, NZ, VEC2, LEN, 9, NZ>(sa, len, j, bufA);
         load_stage_a<TIN, NZ, VEC2, LEN, 0, 4>(sb, len, j, bufB);
@@ -830,8 +854,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         load_stage_a<TIN, NZ, VEC2, LEN, 8, NZ>(sb, len, j, bufB);
         __builtin_amdgcn_sched_barrier(0);
       } else if (work) {
-        windowed(bufA);
-        stage_a<NZ, LEN>(bufA, len, L, j, u);
+        stage_a<TIN, NZ, LEN, WIN>(bufA, len, L, j, u, wv);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
         load_pass(tile + 1, 0, bufA);
@@ -842,8 +865,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           // overlap: pass 1's stage A covers the latency of pass 0's reads
           __builtin_amdgcn_sched_barrier(0);
           VAD_STAMP(2);
-          windowed(bufB);
-          stage_a<NZ, LEN>(bufB, len, L, j, u);
+          stage_a<TIN, NZ, LEN, WIN>(bufB, len, L, j, u, wv);
           __builtin_amdgcn_sched_barrier(0);
           load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
@@ -854,8 +876,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           // variants within 256 VGPRs
           if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
           __builtin_amdgcn_sched_barrier(0);
-          windowed(bufB);
-          stage_a<NZ, LEN>(bufB, len, L, j, u);
+          stage_a<TIN, NZ, LEN, WIN>(bufB, len, L, j, u, wv);
           __builtin_amdgcn_sched_barrier(0);
           load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
@@ -1061,7 +1082,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     const TIN* nb = pair_base(t + 1, lim);
     v2f u[16], col[32];
     VAD_MILESTONE(3);
-    stage_a_at<NZ, LEN, 0>(buf, L, j, u);
+    stage_a_at<TIN, NZ, LEN, 0>(buf, L, j, u);
     __builtin_amdgcn_sched_barrier(0);
     load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
     __builtin_amdgcn_sched_barrier(0);
@@ -1069,7 +1090,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     read_b(L, gscr, col);
     __builtin_amdgcn_sched_barrier(0);
     VAD_MILESTONE(2);
-    stage_a_at<NZ, LEN, HOPC>(buf, L, j, u);
+    stage_a_at<TIN, NZ, LEN, HOPC>(buf, L, j, u);
     __builtin_amdgcn_sched_barrier(0);
     load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
     __builtin_amdgcn_sched_barrier(0);
