@@ -315,31 +315,54 @@ def main():
     ffn_plan = pipe.ffn.plan
     stream = torch.cuda.current_stream()
 
-    gather = LabelGather(F - 5, dev) if world > 1 else None
+    # N > 1: each step's decisions are gathered to rank 0 (RCCL over xGMI).
+    # With nccl the gather of step k runs on RCCL's stream while step k + 1
+    # computes: two label buffers, each reused only after its previous
+    # gather completed (a stream-side wait, no host sync); every gather is
+    # complete before the timed region ends.  gloo (the rehearsal on one GPU)
+    # stages through the host and gathers synchronously.
+    labs = [labels, torch.empty_like(labels)] if world > 1 else [labels]
+    gathers = [LabelGather(F - 5, dev) for _ in labs] if world > 1 else []
+    pend = [None] * len(labs)
+    k_step = [0]
 
     def step():
         # vad_mfcc_ffn with a workspace: the MFCC kernel, then the window
         # features + split-f16 MFMA FFN kernel (the faster of the two clip
         # forms on gfx950; the fused single kernel is timed below)
-        pipe.labels(audio, out=labels)
+        i = k_step[0] % len(labs)
+        k_step[0] += 1
+        if pend[i] is not None:
+            pend[i].wait()
+            pend[i] = None
+        pipe.labels(audio, out=labs[i])
         if world > 1:
-            gather(labels)                                 # RCCL: decisions -> rank 0
+            pend[i] = gathers[i].start(labs[i], async_op=args.backend == "nccl")
+
+    def drain():
+        for i, w in enumerate(pend):
+            if w is not None:
+                w.wait()
+                pend[i] = None
 
     t_w = time.perf_counter()
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     extra = 0
     while time.perf_counter() - t_w < args.min_warmup_s:
         for _ in range(10):
             step()
         extra += 10
+        drain()
         torch.cuda.synchronize()
     if world > 1:  # every rank warms up equally long
         t = torch.tensor([extra], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         for _ in range(int(t.item()) - extra):
             step()
+        drain()
         torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -347,6 +370,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -36,6 +36,24 @@ def _worker(rank, world, port, q):
         got = g(torch.full((4,), rank * 10 + step, dtype=torch.uint8))
         if rank == 0:
             q.put([t.tolist() for t in got])
+    # the asynchronous form bench.py overlaps with the next step (two
+    # buffers, each reused after its handle's wait)
+    gs = [LabelGather(4, torch.device("cpu")) for _ in range(2)]
+    bufs = [torch.empty(4, dtype=torch.uint8) for _ in range(2)]
+    pend = [None, None]
+    for step in range(4):
+        i = step % 2
+        if pend[i] is not None:
+            pend[i].wait()
+            if rank == 0:
+                q.put([t.tolist() for t in gs[i].out])
+        bufs[i].fill_(rank * 10 + step)
+        pend[i] = gs[i].start(bufs[i], async_op=True)
+        assert pend[i] is not None
+    for i in range(2):
+        pend[i].wait()
+        if rank == 0:
+            q.put([t.tolist() for t in gs[i].out])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -50,11 +68,14 @@ def test_gather_labels_gloo(world):
         p.start()
     got = q.get(timeout=120)
     fixed = [q.get(timeout=120) for _ in range(2)]
+    overlapped = [q.get(timeout=120) for _ in range(4)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     assert got == [(i * 3) % 7 for i in range(11)]
     for step, f in enumerate(fixed):
+        assert f == [[r * 10 + step] * 4 for r in range(world)]
+    for step, f in enumerate(overlapped):
         assert f == [[r * 10 + step] * 4 for r in range(world)]
 
 

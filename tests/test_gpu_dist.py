@@ -99,6 +99,27 @@ def _rccl_worker(port, q):
         ok1 = lg.use_gather and len(got) == 1 and bool(torch.equal(got[0], lab))
         var = gather_labels(lab[:12345])
         ok2 = len(var) == 1 and bool(torch.equal(var[0], lab[:12345]))
+        # bench.py's overlapped form: two buffers, the gather of one running
+        # on RCCL's stream while the next labels are written to the other
+        from vad_amd.pipeline import VadPipeline
+        from vad_amd.ffn import FFNClassifier, TOPOLOGY_BL13, random_layers
+        pipe = VadPipeline(FFNClassifier(random_layers(TOPOLOGY_BL13, seed=2)))
+        audio = torch.randn(160 * 20_000 + 241, generator=g, device=dev) * 3000
+        n = pipe.n_frames(audio.numel()) - 5
+        bufs = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        gs = [LabelGather(n, dev) for _ in range(2)]
+        pend = [None, None]
+        ref = pipe.labels(audio).clone()
+        for step in range(6):
+            i = step % 2
+            if pend[i] is not None:
+                pend[i].wait()
+            pipe.labels(audio, out=bufs[i])
+            pend[i] = gs[i].start(bufs[i], async_op=True)
+        for w in pend:
+            w.wait()
+        torch.cuda.synchronize()
+        ok2 = ok2 and all(bool(torch.equal(gg.out[0], ref)) for gg in gs)
         dist.destroy_process_group()
         q.put(("ok", ok1, ok2))
     except Exception as e:

@@ -133,17 +133,28 @@ class LabelGather:
         self.out = [torch.empty((self.n,), dtype=torch.uint8, device=bdev) for _ in range(world)]
 
     def __call__(self, labels: torch.Tensor):
+        self.start(labels, async_op=False)
+        return self.out if self.rank == self.dst else None
+
+    def start(self, labels: torch.Tensor, async_op=True):
+        """Issue the gather; with async_op (device buffers, nccl) return its
+        work handle at once: the collective runs on the backend's stream after
+        the labels are ready, overlapping the caller's next kernels, and
+        `handle.wait()` makes the current stream wait for it (no host sync).
+        The labels and self.out must not be reused before that wait.  Host-
+        staged (gloo) gathers complete before returning (handle None)."""
         if labels.numel() != self.n or labels.dtype != torch.uint8:
             raise ValueError(f"expected {self.n} uint8 labels, got {labels.numel()} {labels.dtype}")
         x = labels.reshape(-1)
+        async_op = bool(async_op) and not self.via_host
         if self.via_host:
             x = x.cpu()
         if self.use_gather:
-            dist.gather(x, self.out if self.rank == self.dst else None, dst=self.global_dst,
-                        group=self.group)
+            work = dist.gather(x, self.out if self.rank == self.dst else None, dst=self.global_dst,
+                               group=self.group, async_op=async_op)
         else:
-            dist.all_gather(self.out, x, group=self.group)
-        return self.out if self.rank == self.dst else None
+            work = dist.all_gather(self.out, x, group=self.group, async_op=async_op)
+        return work if async_op else None
 
 
 def gather_clip_labels(labels: torch.Tensor, shard: ClipShard, dst=0, group=None):
