@@ -410,13 +410,14 @@ def test_analyser_foreign_classifier(torch_cuda, golden, tmp_path):
 # ---------------------------------------------------------------------------
 # streaming batch (config 5) == clip path
 # ---------------------------------------------------------------------------
-def test_stream_batch_matches_clip_path(torch_cuda, golden):
+@pytest.mark.parametrize("S", [1, 5, 24])  # hop kernel blocks hold >= 4 streams: partial blocks too
+def test_stream_batch_matches_clip_path(torch_cuda, golden, S):
     from vad_amd.ffn import FFNClassifier
     from vad_amd.pipeline import VadPipeline
     from vad_amd.stream import StreamBatch
     w = golden("ffn")
     clf = FFNClassifier(layers_from(w, "ref39", 4))
-    S, T = 24, 40
+    T = 40
     clips = [O.synth_clip(160 * (T - 1) + 401, seed=600 + s) for s in range(S)]
     pipe = VadPipeline(clf)
     want = np.stack([pipe.labels(torch_cuda.from_numpy(c).cuda()).cpu().numpy() for c in clips])
