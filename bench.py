@@ -40,6 +40,15 @@ FFN_BYTES_PER_FRAME = 13 * 4 + 1          # MFCC row in + uint8 label out
 # power 768 + sparse mel 888 + log 26 + lifter x DCT 676
 MFCC_FLOPS_PER_FRAME = 13878
 VALU_PEAK_TFS = 157.3          # MI355X_MICROARCH.md: peak FP32 (vector)
+# The MFCC kernel's VALU issue model ("Where the ceiling
+# is"): packed / scalar VALU wave-instructions per frame from its ISA and PMC
+# (profiles/r02b_pmc.txt: 93.1 in all), and the per-SIMD cost of one at two
+# waves per SIMD measured on this part (profiles/r02_valu_rates.txt)
+MFCC_VALU_PACKED_PER_FRAME = 60
+MFCC_VALU_SCALAR_PER_FRAME = 33
+VALU_NS_PACKED_2W = 3.02
+VALU_NS_SCALAR_2W = 1.51
+N_SIMDS = 1024                 # 256 CUs x 4
 
 
 def synth_audio(n_samples, seed, device):
@@ -461,6 +470,17 @@ def main():
                         "peak": VALU_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": MFCC_FLOPS_PER_FRAME * F / (mfcc_ms * 1e-3) / 1e12 / VALU_PEAK_TFS,
                         "flops_per_frame": MFCC_FLOPS_PER_FRAME},
+            # the VALU time those instructions take at the measured rates,
+            # against the kernel's measured launch time
+            "valu_model": {"kernel": "mfcc_kernel",
+                           "packed_per_frame": MFCC_VALU_PACKED_PER_FRAME,
+                           "scalar_per_frame": MFCC_VALU_SCALAR_PER_FRAME,
+                           "ns_packed": VALU_NS_PACKED_2W, "ns_scalar": VALU_NS_SCALAR_2W,
+                           "model_ms": F / N_SIMDS * (MFCC_VALU_PACKED_PER_FRAME * VALU_NS_PACKED_2W
+                                                      + MFCC_VALU_SCALAR_PER_FRAME * VALU_NS_SCALAR_2W) * 1e-6,
+                           "frac_of_launch": F / N_SIMDS * (MFCC_VALU_PACKED_PER_FRAME * VALU_NS_PACKED_2W
+                                                            + MFCC_VALU_SCALAR_PER_FRAME * VALU_NS_SCALAR_2W)
+                           * 1e-6 / mfcc_ms},
             "kernels_ms": {"mfcc_kernel": mfcc_ms, "ffn_kernel": ffn_ms,
                            "ffn_kernel_exact_f32": ffn_f32_ms, "mfcc_ffn_fused_kernel": fused_ms},
             "kernels_ms_pct": {"mfcc_kernel": mfcc_pct, "ffn_kernel": ffn_pct,
