@@ -311,6 +311,7 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   // the previous layer's accumulator rows as the lane holds them.
   std::vector<uint32_t> fragh;
   const bool use_h3 = ref39 || bl13;
+  const bool merge0 = dims[0] <= 16;  // == kMerge0<KS0> of the kernels (bl13)
   if (use_h3) {
     // every layer, output included: the block kernel runs bl13's output
     // layer on the VALU and reads only the hidden layers' slots (the first
@@ -324,6 +325,16 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
               const int i = lane & 15, g = lane >> 4;
               _Float16 h[8];
               for (int q = 0; q < 8; ++q) {
+                if (l == 0 && merge0) {
+                  // <= 16 inputs: one K-step holds both halves of the input,
+                  // k = 0..15 its hi halves, 16..31 its lo halves (ffn_dev.h
+                  // dense_h3 MERGE0); part 0 = [W_hi | W_hi], part 1 = [W_lo | 0]
+                  const int k = 8 * g + q;
+                  const float w = w_at(0, k & 15, 16 * mt + i);
+                  const _Float16 hi = (_Float16)w;
+                  h[q] = part == 0 ? hi : (k < 16 ? (_Float16)(w - (float)hi) : (_Float16)0.f);
+                  continue;
+                }
                 const int k = l == 0 ? 32 * s + 8 * g + q
                                      : 16 * (2 * s + (q >> 2)) + 4 * g + (q & 3);
                 const bool in_range = l == 0 || 2 * s + (q >> 2) < tiles[l - 1];

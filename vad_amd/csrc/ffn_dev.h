@@ -330,13 +330,30 @@ __device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1
 
 // out[mt] = bias + sum_s lo*hi + hi*lo + hi*hi (small terms first) on inputs
 // v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
-template <int TO, int KS, class FB, bool NONNEG = false, class FH>
+template <int TO, int KS, class FB, bool NONNEG = false, bool MERGE0 = false, class FH>
 __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu) {
   const float sc = layer_scale<KS, NONNEG>(v);
   h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
+  // MERGE0 (a first layer of <= 16 inputs, one K-step): lane group g < 2
+  // feeds the hi halves of inputs 8 (g & 1) + q as k = 0..15, g >= 2 their lo
+  // halves as k = 16..31, against A = [W_lo | 0] then [W_hi | W_hi] (the
+  // host's fragments): lo*hi, then hi*hi + hi*lo in one product -- two MFMAs
+  // per tile instead of three
+  const bool lo_half = (__builtin_amdgcn_workitem_id_x() & 63) >= 32;
   auto chain = [&](const f32x4 (&init)[TO], f32x4 (&acc)[TO]) {
+    if constexpr (MERGE0) {
+      static_assert(KS == 1, "merged first layer: one K-step");
+      const h8 bm = lo_half ? bl[0] : bh[0];
+#pragma unroll
+      for (int mt = 0; mt < TO; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A.get(mt, 1)), bm, init[mt], 0, 0, 0);
+#pragma unroll
+      for (int mt = 0; mt < TO; ++mt)
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, A.get(mt, 0)), bm, acc[mt], 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < KS; ++s)
 #pragma unroll
@@ -393,6 +410,12 @@ __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// A first layer of <= 16 inputs (13-64-64-2) carries both halves of its
+// split-f16 inputs in one K-step of 32 (dense_h3 MERGE0; capi.hip builds its
+// fragments to match).
+template <int KS0>
+constexpr bool kMerge0 = 4 * KS0 <= 16;
+
 // Split-f16 shape of a Topo: K-steps per layer and fragment slots.
 template <class TP, int KS0, int T1, int T2, int T3, int T4>
 struct HTopo {
@@ -439,7 +462,7 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)
   using TP = Topo<KS0, T1, T2, T3, T4, NC, NOVL>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
   f32x4 h1[T1];
-  dense_h3<T1, HP::K0, FB>(fh, fb, x0, h1, TP::NL > 1);
+  dense_h3<T1, HP::K0, FB, false, kMerge0<KS0>>(fh, fb, x0, h1, TP::NL > 1);
   if constexpr (TP::NL == 1) return h1[0];
   else if constexpr (TP::NL == 2 && TP::VL) return valu_out_layer<TP, T1, FV>(fv, h1);
   else {
@@ -550,6 +573,20 @@ template <int K0, int IN, int XS, bool MASK>
 __device__ __forceinline__ int wave_tile_operands(const float* __restrict__ X, const int* __restrict__ FL,
                                                   int lane, float (&x0)[K0][8]) {
   const int g = lane >> 4, jw = lane & 15;
+  if constexpr (IN <= 16) {  // kMerge0: lane group g takes inputs 8 (g & 1) + q
+    static_assert(K0 == 1, "one K-step");
+    const v4f* xm = reinterpret_cast<const v4f*>(X + jw * XS + 8 * (g & 1));
+    const v4f lo4 = xm[0], hi4 = xm[1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      x0[0][q] = lo4[q];
+      x0[0][q + 4] = hi4[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (8 + q >= IN) x0[0][q] = 8 * (g & 1) + q < IN ? x0[0][q] : 0.f;
+    return FL[jw];
+  }
   const v4f* xr = reinterpret_cast<const v4f*>(X + jw * XS + 8 * g);
 #pragma unroll
   for (int s = 0; s < K0; ++s) {

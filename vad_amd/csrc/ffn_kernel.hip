@@ -240,7 +240,9 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
     if constexpr (H3) {
       // windows past nwin read stale (finite) features: computed, not stored
       float x0[HP::K0][8];
-      const v4f* xr = reinterpret_cast<const v4f*>(Xb + wl * kXStride + 8 * g);
+      // kMerge0 (<= 16 inputs): lane group g takes inputs 8 (g & 1) + q
+      constexpr bool M0 = kMerge0<KS0>;
+      const v4f* xr = reinterpret_cast<const v4f*>(Xb + wl * kXStride + 8 * (M0 ? (g & 1) : g));
 #pragma unroll
       for (int s = 0; s < HP::K0; ++s) {
         const v4f lo4 = xr[8 * s], hi4 = xr[8 * s + 1];
@@ -249,6 +251,11 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
           x0[s][q] = lo4[q];
           x0[s][q + 4] = hi4[q];
         }
+      }
+      if constexpr (M0) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (8 + q >= 4 * KS0) x0[0][q] = 8 * (g & 1) + q < 4 * KS0 ? x0[0][q] : 0.f;
       }
       if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
       else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(FragRegs{fh}, (const float*)fb, (const float*)fv, x0);
