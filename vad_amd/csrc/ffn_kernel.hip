@@ -252,10 +252,10 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
           x0[s][q + 4] = hi4[q];
         }
       }
-      if constexpr (M0) {
+      if constexpr (M0) {  // the 13 analyser inputs; columns 13..15 zeroed in registers
 #pragma unroll
         for (int q = 0; q < 8; ++q)
-          if (8 + q >= 4 * KS0) x0[0][q] = 8 * (g & 1) + q < 4 * KS0 ? x0[0][q] : 0.f;
+          if (8 + q >= 13) x0[0][q] = 8 * (g & 1) + q < 13 ? x0[0][q] : 0.f;
       }
       if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
       else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(FragRegs{fh}, (const float*)fb, (const float*)fv, x0);
