@@ -34,6 +34,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0          # MI355X_MICROARCH.md: measured device copy (SURVEY 8(d) asks for both)
 MFCC_BYTES_PER_FRAME = 160 * 4 + 13 * 4   # new samples in + 13 fp32 out
 FFN_BYTES_PER_FRAME = 13 * 4 + 1          # MFCC row in + uint8 label out
 # SURVEY 8(d) algorithmic flops per frame of the MFCC kernel: FFT 11,520 +
@@ -461,6 +462,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac_vs_measured_copy": achieved / HBM_COPY_GBS,
                          "algorithmic_bytes_per_launch": dom_bytes * F,
                          "avg_launch_ms": dom_ms},
             # the MFCC kernel sits at the fp32 ridge (~20 flop/B): its VALU
