@@ -28,13 +28,14 @@ extern "C" {
 
 #define VAD_MAX_FILTERS 64
 #define VAD_MAX_MFCC 16
-#define VAD_MAX_TAPS 4096
+#define VAD_MAX_TAPS 16384
 #define VAD_FFT_N 512
+#define VAD_MAX_FFT_N 8192  /* other fft_n (2..8192) run a direct-DFT path */
 #define VAD_MAX_FFN_LAYERS 4
 
 #define VAD_OK 0
 #define VAD_EINVAL (-1)        /* bad argument (null, negative size, ...) */
-#define VAD_EUNSUPPORTED (-2)  /* valid for the reference, not built here (fft_n != 512, ...) */
+#define VAD_EUNSUPPORTED (-2)  /* valid for the reference, not built here (see each entry) */
 #define VAD_ENOMEM (-3)
 #define VAD_ERCCL (-4)         /* RCCL returned an error: vad_rccl_error_string() */
 
@@ -54,7 +55,13 @@ int64_t vad_n_frames(int64_t n_samples, int32_t frame_size, int32_t hop);
  * filterbank from get_mel_filterbanks (mfcc.py:39-56, built on the host in
  * fp64 exactly as the reference does), the MFCC count (mfcc.py:76 [:mfcc_n])
  * and the lifter length (mfcc.py:85, L=22 in every reference call).
- * fft_n must be 512 (mfcc.py:61 with the reference's only value, config.py:27).
+ * fft_n: any length 2..VAD_MAX_FFT_N, as np.fft.fft(frame, fft_n) takes
+ * (mfcc.py:61; the filterbank is then (n_filters, fft_n / 2)).  512, the
+ * reference's only value (config.py:27, sklearn_analyser.py:21), runs the
+ * radix-16 x 16 kernels; other lengths a direct DFT with fp64 accumulation
+ * (vad_mfcc_f32 / _i16, vad_spec_*, vad_mfcc_from_spec_f32, the workspace
+ * form of vad_mfcc_ffn and vad_stream_step; the fused clip kernel, the
+ * analysis window and vad_stream_hop return VAD_EUNSUPPORTED for them).
  * ------------------------------------------------------------------------- */
 int vad_mfcc_plan_create(const double* filterbank_host, int32_t n_filters, int32_t fft_n,
                          int32_t mfcc_n, int32_t lifter_L, vad_mfcc_plan** out);

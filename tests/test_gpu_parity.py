@@ -623,3 +623,69 @@ def test_analyser_with_pickled_sklearn_tree(torch_cuda, golden, tmp_path):
     for fr in stream:
         r1, r2 = an_gpu.feed_frame(fr), an_host.feed_frame(fr)
         assert (r1 is None and r2 is None) or (r1 is r2)
+
+
+# ---------------------------------------------------------------------------
+# fft_n other than 512 (mfcc.py:59-61 takes any length; every reference call
+# site passes 512): the direct-DFT path, against the oracle's pocketfft
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("fft_n,n_filters", [(256, 16), (400, 26), (401, 26), (1024, 26), (2048, 40),
+                                              (8192, 26)])
+def test_other_fft_lengths(torch_cuda, fft_n, n_filters):
+    torch = torch_cuda
+    from vad_amd import mfcc as M
+    from vad_amd.plan import MfccPlan
+    rng = np.random.default_rng(fft_n)
+    fb = O.get_mel_filterbanks(300, 8000, fft_n, n_filters, 16000)
+    assert np.isfinite(fb).all()
+    for L in (400, 300, fft_n + 100):  # zero-padded and truncated frames
+        frame = np.round(rng.standard_normal(L) * 3000).astype(np.float32)
+        s = M.get_spec_mag(frame, fft_n)
+        ref = O.get_spec_mag(frame, fft_n)
+        assert s.dtype == np.float32 and s.shape == ref.shape == (fft_n // 2,)
+        assert frame_rel(s, ref) <= SPEC_TOL
+        assert_mfcc_close(M.get_mfcc(frame, fft_n, fb, 13)[None], O.get_mfcc(frame, fft_n, fb, 13)[None])
+        assert_mfcc_close(M.get_mfcc_from_spec(ref, fb, 13)[None], O.get_mfcc_from_spec(ref, fb, 13)[None])
+    # a clip through a plan: every frame, fp32 and int16 PCM (identical)
+    clip = O.synth_clip(O.samples_for_frames(300), seed=fft_n)
+    p = MfccPlan(fb, 13, fft_n)
+    assert p.variant == 0
+    a = torch.from_numpy(clip).cuda()
+    got = p.clip_mfcc(a).cpu().numpy()
+    assert_mfcc_close(got, O.mfcc_batch(clip, fb, fft_n=fft_n))
+    assert np.array_equal(p.clip_mfcc(a.to(torch.int16)).cpu().numpy(), got)
+
+
+def test_other_fft_length_pipeline(torch_cuda):
+    """A 1024-point MFCC config through VadPipeline (workspace form) and the
+    three-kernel streaming step; the fused kernel and the hop kernel are the
+    fft_n = 512 pipeline and say so."""
+    torch = torch_cuda
+    from vad_amd import _lib
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.stream import StreamBatch
+    layers = random_layers(TOPOLOGY_BL13, seed=9)
+    pipe = VadPipeline(FFNClassifier(layers), cfg=MfccConfig(fft_n=1024))
+    clip = O.synth_clip(O.samples_for_frames(3000), seed=91)
+    lab = pipe.labels(torch.from_numpy(clip).cuda()).cpu().numpy()
+    fb = O.get_mel_filterbanks(300, 8000, 1024, 26, 16000)
+    x = O.analyser_features_fast(O.mfcc_batch(clip, fb, fft_n=1024))[:, :13]
+    sure = O.ffn_margin(x, layers) > MARGIN_TOL
+    np.testing.assert_array_equal(lab[sure], O.ffn_labels(x, layers)[sure])
+    assert not pipe.fusable
+    with pytest.raises(RuntimeError):  # VadError: VAD_EUNSUPPORTED
+        pipe.labels(torch.from_numpy(clip).cuda(), fused=True)
+    # the three-kernel streaming step runs the same path; 3 identical streams
+    sb = StreamBatch(3, FFNClassifier(layers), cfg=MfccConfig(fft_n=1024), kernel="three")
+    sb.prime(torch.from_numpy(np.stack([clip[:240]] * 3)).cuda())
+    outs = [sb.step(torch.from_numpy(np.stack([clip[240 + 160 * t: 400 + 160 * t]] * 3)).cuda())
+            .cpu().numpy().copy() for t in range(12)]
+    for t in range(5, 12):
+        if sure[t - 5]:
+            assert outs[t].tolist() == [lab[t - 5]] * 3
+    hop = StreamBatch(3, FFNClassifier(layers), cfg=MfccConfig(fft_n=1024), kernel="hop")
+    hop.prime(torch.from_numpy(np.stack([clip[:240]] * 3)).cuda())
+    with pytest.raises(RuntimeError):
+        hop.step(torch.from_numpy(np.stack([clip[240:400]] * 3)).cuda())

@@ -17,7 +17,8 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libvad_amd.so")
 ARCH = os.environ.get("VAD_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["capi.hip", "mfcc_kernel.hip", "ffn_kernel.hip", "tree_kernel.hip",
-           "dataset_kernel.hip", "csv_format.hip", "simple_kernel.hip", "stream_kernel.hip", "rccl.hip"]
+           "dataset_kernel.hip", "csv_format.hip", "simple_kernel.hip", "stream_kernel.hip", "rccl.hip",
+           "spec_generic.hip"]
 # per-translation-unit code-generation flags: the FFT's packed-fp32 chains
 # run ~5% faster under the ILP-oriented machine scheduler (fewer dependent
 # pairs back to back, i.e. fewer hazard s_nops and stalls)
@@ -31,6 +32,7 @@ UNIT_FLAGS = {
     "stream_kernel.hip": [],
     "capi.hip": [],
     "rccl.hip": [],
+    "spec_generic.hip": [],
 }
 
 

@@ -22,6 +22,10 @@ struct vad_mfcc_plan {
   float* hop_blob;   // stream_hop_kernel's tables, one contiguous block (LDS-staged per launch)
   int hop_blob_n;    // floats (a multiple of 4)
   int n_taps;
+  int fft_n;         // 512, or another length run by spec_generic.hip
+  int bins;          // fft_n / 2 spectrum bins kept (mfcc.py:61)
+  double2* tw_gen;   // exp(-2 pi i m / fft_n), m < fft_n (other lengths only)
+  bool generic() const { return fft_n != kFftN; }
 };
 
 // Does the runtime plan equal compile-time table T (taps, ranges, DCT rows)?
@@ -67,7 +71,7 @@ int64_t vad_n_frames(int64_t n_samples, int32_t frame_size, int32_t hop) {
 int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int32_t mfcc_n,
                          int32_t lifter_L, vad_mfcc_plan** out) {
   if (!fb || !out || n_filters <= 0 || mfcc_n <= 0) return VAD_EINVAL;
-  if (fft_n != VAD_FFT_N) return VAD_EUNSUPPORTED;
+  if (fft_n < 2 || fft_n > VAD_MAX_FFT_N) return VAD_EUNSUPPORTED;
   if (n_filters > VAD_MAX_FILTERS || mfcc_n > VAD_MAX_MFCC || mfcc_n > n_filters)
     return VAD_EUNSUPPORTED;
   vad_mfcc_plan* p = (vad_mfcc_plan*)calloc(1, sizeof(vad_mfcc_plan));
@@ -75,22 +79,27 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
   MfccDev& h = p->host;
   h.n_filters = n_filters;
   h.mfcc_n = mfcc_n;
+  p->fft_n = fft_n;
+  p->bins = fft_n / 2;
+  const int bins = p->bins;
   // filterbank rows -> contiguous tap ranges [first non-zero, last non-zero]
   // (NaN counts as non-zero: a degenerate reference filter stays NaN).
   int off = 0;
   std::vector<int> cost(n_filters);
   for (int m = 0; m < n_filters; ++m) {
-    const double* row = fb + (size_t)m * kBins;
+    const double* row = fb + (size_t)m * bins;
     int lo = -1, hi = -1;
-    for (int k = 0; k < kBins; ++k)
+    for (int k = 0; k < bins; ++k)
       if (row[k] != 0.0) { if (lo < 0) lo = k; hi = k; }
     const int n = lo < 0 ? 0 : hi - lo + 1;
     if (off + n > VAD_MAX_TAPS) { free(p); return VAD_EUNSUPPORTED; }
     h.f_lo[m] = lo < 0 ? 0 : lo;
     h.f_len[m] = n;
     h.f_off[m] = off;
-    // x 2^-20: the FFT path produces |2X|^2 and P = |X/512|^2 = |2X|^2 2^-20 (exact)
-    for (int t = 0; t < n; ++t) h.taps[off + t] = (float)row[lo + t] * 0x1p-20f;
+    // x 2^-20: the FFT path produces |2X|^2 and P = |X/512|^2 = |2X|^2 2^-20
+    // (exact); the direct DFT of other lengths produces P itself
+    const float tsc = p->generic() ? 1.f : 0x1p-20f;
+    for (int t = 0; t < n; ++t) h.taps[off + t] = (float)row[lo + t] * tsc;
     off += n;
     cost[m] = n + 8;  // taps + (==0 -> eps) + log10, in VALU-op units
   }
@@ -129,7 +138,17 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     const double a = -2.0 * M_PI * k / 512.0;
     h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
   }
-  p->spec = p->table_spec = matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
+  p->spec = p->table_spec = p->generic() ? 0 : matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
+  if (p->generic()) {
+    std::vector<double2> tw(fft_n);
+    for (int m = 0; m < fft_n; ++m) {
+      const double a = -2.0 * M_PI * (double)m / (double)fft_n;
+      tw[m] = make_double2(cos(a), sin(a));
+    }
+    hipError_t e = hipMalloc((void**)&p->tw_gen, tw.size() * sizeof(double2));
+    if (e == hipSuccess) e = hipMemcpy(p->tw_gen, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(p->tw_gen); free(p); return (int)e; }
+  }
   // the streaming hop kernel's tables as one block: W512^k (256 complex),
   // f_lo / f_len / f_off (as int bits), the taps, the DCT rows at stride nf
   p->n_taps = off;
@@ -144,11 +163,13 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
   p->hop_blob_n = (int)blob.size();
   hipError_t e = hipMalloc((void**)&p->hop_blob, blob.size() * sizeof(float));
   if (e == hipSuccess) e = hipMemcpy(p->hop_blob, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(p->hop_blob); free(p); return (int)e; }
+  if (e != hipSuccess) { (void)hipFree(p->hop_blob); (void)hipFree(p->tw_gen); free(p); return (int)e; }
   e = hipMalloc((void**)&p->dev, sizeof(MfccDev));
-  if (e != hipSuccess) { (void)hipFree(p->hop_blob); free(p); return (int)e; }
+  if (e != hipSuccess) { (void)hipFree(p->hop_blob); (void)hipFree(p->tw_gen); free(p); return (int)e; }
   e = hipMemcpy(p->dev, &h, sizeof(MfccDev), hipMemcpyHostToDevice);
-  if (e != hipSuccess) { (void)hipFree(p->dev); (void)hipFree(p->hop_blob); free(p); return (int)e; }
+  if (e != hipSuccess) {
+    (void)hipFree(p->dev); (void)hipFree(p->hop_blob); (void)hipFree(p->tw_gen); free(p); return (int)e;
+  }
   *out = p;
   return VAD_OK;
 }
@@ -157,6 +178,7 @@ int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
   if (!p) return VAD_OK;
   (void)hipFree(p->dev);
   (void)hipFree(p->hop_blob);
+  (void)hipFree(p->tw_gen);
   free(p);
   return VAD_OK;
 }
@@ -165,6 +187,7 @@ int32_t vad_mfcc_plan_variant(const vad_mfcc_plan* p) { return p ? p->spec : -1;
 
 int vad_mfcc_plan_set_window(vad_mfcc_plan* p, const float* window_host, int32_t len) {
   if (!p) return VAD_EINVAL;
+  if (p->generic()) return VAD_EUNSUPPORTED;  // the window multiplies the radix-16 kernels' frames
   if (window_host && (len <= 0 || len > kFftN)) return VAD_EINVAL;
   for (int t = 0; t < kFftN; ++t) p->host.window[t] = window_host && t < len ? window_host[t] : 0.f;
   const hipError_t e = hipMemcpy(p->dev->window, p->host.window, sizeof(p->host.window), hipMemcpyHostToDevice);
@@ -185,6 +208,7 @@ int vad_mfcc_plan_set_variant(vad_mfcc_plan* p, int32_t variant) {
   if (!p) return VAD_EINVAL;
   if (p->spec == kSpecWindow) return VAD_EINVAL;  // windowed plans run the runtime-table kernel
   if (variant == 0) { p->spec = 0; return VAD_OK; }
+  if (p->generic()) return VAD_EINVAL;
   if (variant == 1 && matches_table<Mel26>(p->host)) { p->spec = 1; return VAD_OK; }
   if (variant == 2 && matches_table<Mel40>(p->host)) { p->spec = 2; return VAD_OK; }
   return VAD_EINVAL;
@@ -202,6 +226,8 @@ int vad_spec_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
                  float* spec, void* stream) {
   int r = check_frames(p, src, stride, len, n, spec);
   if (r || n == 0) return r;
+  if (p->generic()) return (int)launch_generic(1, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, spec,
+                                               (hipStream_t)stream);
   return (int)launch_mfcc(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
 }
 
@@ -209,6 +235,8 @@ int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
                  float* mfcc, void* stream) {
   int r = check_frames(p, src, stride, len, n, mfcc);
   if (r || n == 0) return r;
+  if (p->generic()) return (int)launch_generic(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
+                                               (hipStream_t)stream);
   return (int)launch_mfcc(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
@@ -216,6 +244,8 @@ int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
                  float* spec, void* stream) {
   int r = check_frames(p, src, stride, len, n, spec);
   if (r || n == 0) return r;
+  if (p->generic()) return (int)launch_generic_i16(1, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, spec,
+                                                   (hipStream_t)stream);
   return (int)launch_mfcc_i16(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
 }
 
@@ -223,13 +253,18 @@ int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
                  float* mfcc, void* stream) {
   int r = check_frames(p, src, stride, len, n, mfcc);
   if (r || n == 0) return r;
+  if (p->generic()) return (int)launch_generic_i16(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
+                                                   (hipStream_t)stream);
   return (int)launch_mfcc_i16(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
                            void* stream) {
-  int r = check_frames(p, spec, kBins, kBins, n, mfcc);
+  if (!p) return VAD_EINVAL;
+  int r = check_frames(p, spec, p->bins, p->bins, n, mfcc);
   if (r || n == 0) return r;
+  if (p->generic()) return (int)launch_generic(2, p->dev, spec, p->bins, p->bins, n, p->fft_n, p->tw_gen, mfcc,
+                                               (hipStream_t)stream);
   return (int)launch_mfcc(2, p->dev, p->spec, spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
 }
 
@@ -605,13 +640,20 @@ static int mfcc_ffn_entry(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, co
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (!workspace) {
+    if (plan->generic()) return VAD_EUNSUPPORTED;  // the fused kernel is the fft_n = 512 pipeline
     if (!mfcc_ffn_fusable(plan->spec, ffn->net, frame_size, hop, audio, tin_bytes)) return VAD_EINVAL;
     return (int)launch_mfcc_ffn(plan->dev, ffn->net, audio, tin_bytes, f, mode, labels, st);
   }
   const size_t need = (size_t)f * plan->host.mfcc_n * sizeof(float);
   if (workspace_bytes < need) return VAD_EINVAL;
   float* mf = (float*)workspace;
-  if (tin_bytes == 2)
+  if (plan->generic() && tin_bytes == 2)
+    VAD_TRY(launch_generic_i16(0, plan->dev, (const int16_t*)audio, hop, frame_size, f, plan->fft_n, plan->tw_gen,
+                               mf, st));
+  else if (plan->generic())
+    VAD_TRY(launch_generic(0, plan->dev, (const float*)audio, hop, frame_size, f, plan->fft_n, plan->tw_gen, mf,
+                           st));
+  else if (tin_bytes == 2)
     VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, (const int16_t*)audio, hop, frame_size, f, mf, st));
   else
     VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, (const float*)audio, hop, frame_size, f, mf, st));
@@ -656,6 +698,7 @@ int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* fr
   if (n_streams == 0) return VAD_OK;
   if (!frames || !hop || !ring || !count || !labels) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
+  if (plan->generic()) return VAD_EUNSUPPORTED;  // its FFT is the 256-point Stockham of fft_n = 512
   return (int)launch_stream_hop(plan->dev, plan->hop_blob, plan->hop_blob_n, plan->host.n_filters, plan->n_taps,
                                 ffn->net, frames, frame_stride, frame_len, hop, hop_stride, hop_len,
                                 n_streams, plan->host.mfcc_n, ring, count, labels, (hipStream_t)stream);
@@ -669,7 +712,11 @@ int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const fl
   if (!frames || !ring || !count || !labels || !mfcc_scratch) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
+  if (plan->generic())
+    VAD_TRY(launch_generic(0, plan->dev, frames, frame_stride, frame_len, n_streams, plan->fft_n, plan->tw_gen,
+                           mfcc_scratch, st));
+  else
+    VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
   return (int)launch_stream_ffn(ffn->net, mfcc_scratch, ring, count, n_streams, plan->host.mfcc_n,
                                 labels, st);
 }

@@ -18,6 +18,7 @@ constexpr int kBins = kFftN / 2;    // bins 0..255 kept (Nyquist dropped)
 constexpr int kMaxFilters = VAD_MAX_FILTERS;
 constexpr int kMaxCoefs = VAD_MAX_MFCC;
 constexpr int kMaxTaps = VAD_MAX_TAPS;
+constexpr int kMaxGenericFft = VAD_MAX_FFT_N;  // other FFT lengths: spec_generic.hip
 
 // Device-resident MFCC plan.  Read by every wave through scalar loads
 // (the indices are wave-uniform), so it lives in plain global memory.
@@ -108,6 +109,12 @@ hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const flo
                               int hlen, int64_t n_streams, hipStream_t st);
 hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,
                               hipStream_t st);
+// any fft_n other than 512 (spec_generic.hip): mode 0 frames -> MFCC,
+// 1 frames -> spectra, 2 spectra -> MFCC; tw = exp(-2 pi i m / fft_n), fp64
+hipError_t launch_generic(int mode, const MfccDev* plan, const float* src, int64_t stride, int len, int64_t n,
+                          int fft_n, const double2* tw, float* out, hipStream_t st);
+hipError_t launch_generic_i16(int mode, const MfccDev* plan, const int16_t* src, int64_t stride, int len,
+                              int64_t n, int fft_n, const double2* tw, float* out, hipStream_t st);
 hipError_t launch_features(const float* mfcc, int64_t n_rows, int mfcc_n, int mode, float* out,
                            hipStream_t st);
 hipError_t launch_simple_features(const float* frames, int64_t n_frames, int frame_len,

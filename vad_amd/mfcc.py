@@ -75,7 +75,7 @@ def plan_for(filterbank, mfcc_n=13, fft_n=512):
     return p
 
 
-_spec_plan = None
+_spec_plans = {}
 
 
 def _frame_tensor(frame):
@@ -86,14 +86,16 @@ def _frame_tensor(frame):
 
 
 def get_spec_mag(frame, fft_n=512):
-    """mfcc.py:59-61 -- |fft(frame, fft_n)[:fft_n/2] / fft_n|^2 as float32 (256,)."""
-    global _spec_plan
-    if int(fft_n) != 512:
-        raise NotImplementedError("this build implements the reference's fft_n = 512 only")
-    if _spec_plan is None:
-        _spec_plan = MfccPlan(get_mel_filterbanks(300, 8000, 512, 26, 16000), 13, 512)
+    """mfcc.py:59-61 -- |fft(frame, fft_n)[:fft_n/2] / fft_n|^2 as float32 (fft_n // 2,).
+
+    fft_n = 512 (the reference's only value) runs the radix-16 kernels, any
+    other length (2..8192) a direct DFT with fp64 accumulation."""
+    n = int(fft_n)
+    p = _spec_plans.get(n)
+    if p is None:
+        p = _spec_plans[n] = MfccPlan(get_mel_filterbanks(300, 8000, n, 26, 16000), 13, n)
     x = _frame_tensor(frame)
-    return _spec_plan.spec(x, frame_len=x.numel(), frame_stride=x.numel(), n=1)[0].cpu().numpy()
+    return p.spec(x, frame_len=x.numel(), frame_stride=x.numel(), n=1)[0].cpu().numpy()
 
 
 def get_mfcc(frame, fft_n, filterbank, mfcc_n):
@@ -105,11 +107,13 @@ def get_mfcc(frame, fft_n, filterbank, mfcc_n):
 
 
 def get_mfcc_from_spec(spec, filterbank, mfcc_n):
-    """mfcc.py:72-78 -- MFCCs of one (256,) spectrum (or a (n, 256) batch), float64."""
+    """mfcc.py:72-78 -- MFCCs of one (B,) spectrum (or a (n, B) batch), float64;
+    B = the filterbank's columns (256 for the reference's fft_n = 512)."""
     s = np.ascontiguousarray(np.asarray(spec, dtype=np.float32))
     single = s.ndim == 1
     t = torch.from_numpy(s.reshape(-1, s.shape[-1])).cuda()
-    out = plan_for(filterbank, mfcc_n).from_spec(t).cpu().numpy().astype(np.float64)
+    fb = np.asarray(filterbank)
+    out = plan_for(fb, mfcc_n, 2 * fb.shape[1]).from_spec(t).cpu().numpy().astype(np.float64)
     return out[0] if single else out
 
 
