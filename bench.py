@@ -258,7 +258,11 @@ def secondary_configs(dev, reps=60):
             "note": "6 rotated 64 MB clips (384 MB working set)"}
     del clips
     S = 512
-    for name, kernel, graph in (("hop_kernel", "hop", False), ("three_kernel_hipgraph", "three", True)):
+    # BASELINE configs[4] names a hipGraph per hop: the one-kernel hop both
+    # launched directly and captured (the graph's input copy included), and
+    # the three-kernel form captured
+    for name, kernel, graph in (("hop_kernel", "hop", False), ("hop_kernel_hipgraph", "hop", True),
+                                ("three_kernel_hipgraph", "three", True)):
         sb = StreamBatch(S, FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)), kernel=kernel)
         g = torch.Generator(device=dev).manual_seed(500)
         sb.prime(torch.randn((S, 240), generator=g, device=dev) * 1000)
