@@ -28,6 +28,14 @@ struct vad_mfcc_plan {
   bool generic() const { return fft_n != kFftN; }
 };
 
+// The spec a launch passes: a windowed plan whose bank is a compiled one
+// says which (kSpecWindow26 / 40), so the reference framing keeps the
+// generated mel code; vad_mfcc_plan_variant still reports kSpecWindow.
+static int launch_spec(const vad_mfcc_plan* p) {
+  if (p->spec != kSpecWindow) return p->spec;
+  return p->table_spec == 1 ? kSpecWindow26 : p->table_spec == 2 ? kSpecWindow40 : kSpecWindow;
+}
+
 // Does the runtime plan equal compile-time table T (taps, ranges, DCT rows)?
 template <class T>
 static bool matches_table(const MfccDev& h) {
@@ -228,7 +236,7 @@ int vad_spec_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic(1, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, spec,
                                                (hipStream_t)stream);
-  return (int)launch_mfcc(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
+  return (int)launch_mfcc(1, p->dev, launch_spec(p), src, stride, len, n, spec, (hipStream_t)stream);
 }
 
 int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32_t len, int64_t n,
@@ -237,7 +245,7 @@ int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
                                                (hipStream_t)stream);
-  return (int)launch_mfcc(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
 int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,
@@ -246,7 +254,7 @@ int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic_i16(1, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, spec,
                                                    (hipStream_t)stream);
-  return (int)launch_mfcc_i16(1, p->dev, p->spec, src, stride, len, n, spec, (hipStream_t)stream);
+  return (int)launch_mfcc_i16(1, p->dev, launch_spec(p), src, stride, len, n, spec, (hipStream_t)stream);
 }
 
 int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,
@@ -255,7 +263,7 @@ int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic_i16(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
                                                    (hipStream_t)stream);
-  return (int)launch_mfcc_i16(0, p->dev, p->spec, src, stride, len, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc_i16(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream);
 }
 
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
@@ -265,7 +273,7 @@ int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n,
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic(2, p->dev, spec, p->bins, p->bins, n, p->fft_n, p->tw_gen, mfcc,
                                                (hipStream_t)stream);
-  return (int)launch_mfcc(2, p->dev, p->spec, spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc(2, p->dev, launch_spec(p), spec, kBins, kBins, n, mfcc, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -654,9 +662,9 @@ static int mfcc_ffn_entry(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, co
     VAD_TRY(launch_generic(0, plan->dev, (const float*)audio, hop, frame_size, f, plan->fft_n, plan->tw_gen, mf,
                            st));
   else if (tin_bytes == 2)
-    VAD_TRY(launch_mfcc_i16(0, plan->dev, plan->spec, (const int16_t*)audio, hop, frame_size, f, mf, st));
+    VAD_TRY(launch_mfcc_i16(0, plan->dev, launch_spec(plan), (const int16_t*)audio, hop, frame_size, f, mf, st));
   else
-    VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, (const float*)audio, hop, frame_size, f, mf, st));
+    VAD_TRY(launch_mfcc(0, plan->dev, launch_spec(plan), (const float*)audio, hop, frame_size, f, mf, st));
   return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
 }
 
@@ -716,7 +724,7 @@ int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const fl
     VAD_TRY(launch_generic(0, plan->dev, frames, frame_stride, frame_len, n_streams, plan->fft_n, plan->tw_gen,
                            mfcc_scratch, st));
   else
-    VAD_TRY(launch_mfcc(0, plan->dev, plan->spec, frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
+    VAD_TRY(launch_mfcc(0, plan->dev, launch_spec(plan), frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
   return (int)launch_stream_ffn(ffn->net, mfcc_scratch, ring, count, n_streams, plan->host.mfcc_n,
                                 labels, st);
 }

@@ -295,11 +295,16 @@ __device__ __forceinline__ void load_chunks(const TIN* __restrict__ base, int li
 }
 
 // stage A of the frame whose chunk n1 is buf[OFF + n1]
-template <typename TIN, int NZ, int LEN, int OFF, int NB>
+template <typename TIN, int NZ, int LEN, int OFF, int NB, bool WIN = false>
 __device__ __forceinline__ void stage_a_at(const v2f (&buf)[NB], const LaneConsts& L, int j,
-                                           v2f (&u)[16]) {
+                                           v2f (&u)[16], const float* wv = nullptr) {
 #pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[OFF + n]);
+  for (int n = 0; n < NZ; ++n) {
+    u[n] = Samples<TIN>::cvt(buf[OFF + n]);
+    // optional analysis window (not in the reference, mfcc.py:59-61): the
+    // frame-relative samples 32 n + 2 j, + 1 of this lane
+    if constexpr (WIN) u[n] = u[n] * (v2f){wv[2 * n], wv[2 * n + 1]};
+  }
   pad_stage_a<NZ, LEN, 16>(LEN, j, u);
   pk::dft16<NZ>(u);
 #pragma unroll
@@ -629,6 +634,14 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     v2f* gscr = scr + grp * kGroupScratch;
     LaneConsts L;
     lane_consts(plan, j, L);
+    float wv[WIN ? 2 * NZ : 1];  // the optional window's samples of this lane (both frames)
+    if constexpr (WIN) {
+#pragma unroll
+      for (int n1 = 0; n1 < NZ; ++n1) {
+        wv[2 * n1] = plan->window[32 * n1 + 2 * j];
+        wv[2 * n1 + 1] = plan->window[32 * n1 + 2 * j + 1];
+      }
+    }
     const int64_t flast = n_frames - 1;
     // frame-granular, balanced runs: workgroup b owns frames
     // [b F / G, (b + 1) F / G) in 64-frame tiles of its own; in a last,
@@ -694,7 +707,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         v2f u[16], col[32];
         VAD_STAMP(0);
         VAD_MILESTONE(3);
-        stage_a_at<TIN, NZ, LEN, 0>(buf, L, j, u);
+        stage_a_at<TIN, NZ, LEN, 0, NB, WIN>(buf, L, j, u, wv);
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
         load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
@@ -705,7 +718,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         VAD_STAMP(2);
         VAD_MILESTONE(2);
         // pass 1's stage A covers the latency of pass 0's transpose reads
-        stage_a_at<TIN, NZ, LEN, HOPC>(buf, L, j, u);
+        stage_a_at<TIN, NZ, LEN, HOPC, NB, WIN>(buf, L, j, u, wv);
         __builtin_amdgcn_sched_barrier(0);
         load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
@@ -1173,6 +1186,16 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
   const int used = len < kFftN ? len : kFftN;
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
                     ((stride & 1) == 0) && ((used & 1) == 0);
+  if ((spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40) && used == 400 && vec2 &&
+      stride == 160 && kPairFrames) {
+    // optional analysis window at the reference framing: the paired-frame
+    // kernel with the window applied in its stage A (and the generated mel
+    // code when the bank is a compiled one)
+    if (spec == kSpecWindow26) return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5, true>(plan, src, stride, len, n, out, st);
+    if (spec == kSpecWindow40) return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5, true>(plan, src, stride, len, n, out, st);
+    return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5, true>(plan, src, stride, len, n, out, st);
+  }
+  if (spec == kSpecWindow26 || spec == kSpecWindow40) spec = kSpecWindow;
   if (spec == kSpecWindow) {  // optional analysis window: the runtime-table kernel with WIN
     if (used <= 32 * 13)
       return vec2 ? launch_t<TIN, MODE, 13, true, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
@@ -1216,10 +1239,14 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src
   switch (mode) {
     case kAudioToMfcc: return launch_m<float, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
     case kAudioToSpec:
-      return launch_m<float, kAudioToSpec>(plan, spec == kSpecWindow ? kSpecWindow : 0, src, stride, len, n, out, st);
+      return launch_m<float, kAudioToSpec>(plan, spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40
+                                                     ? kSpecWindow : 0, src, stride, len, n, out, st);
     default:
+      // spectra in: the window was applied before the FFT
+      if (spec == kSpecWindow26) spec = 1;
+      if (spec == kSpecWindow40) spec = 2;
       if (spec == 1) return launch_t<float, kSpecToMfcc, 13, false, 0, 1>(plan, src, 0, 0, n, out, st);
-      if (spec == kSpecWindow) spec = 0;  // spectra in: the window was applied before the FFT
+      if (spec == kSpecWindow) spec = 0;
       if (spec == 2) return launch_t<float, kSpecToMfcc, 13, false, 0, 2>(plan, src, 0, 0, n, out, st);
       return launch_t<float, kSpecToMfcc, 13, false, 0>(plan, src, 0, 0, n, out, st);
   }
@@ -1229,7 +1256,8 @@ hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_
                            int64_t stride, int len, int64_t n, float* out, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (mode == kAudioToSpec)
-    return launch_m<int16_t, kAudioToSpec>(plan, spec == kSpecWindow ? kSpecWindow : 0, src, stride, len, n, out, st);
+    return launch_m<int16_t, kAudioToSpec>(plan, spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40
+                                                       ? kSpecWindow : 0, src, stride, len, n, out, st);
   return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
 }
 

@@ -39,6 +39,11 @@ struct MfccDev {
 
 // plan variant of a plan with an analysis window (vad_mfcc_plan_set_window)
 constexpr int kSpecWindow = 3;
+// the launch-time form of a windowed plan whose filterbank is also the
+// compiled 26 / 40-filter bank (capi.hip launch_spec): the reference framing
+// then runs the paired-frame kernel with those tables and the window
+constexpr int kSpecWindow26 = 5;
+constexpr int kSpecWindow40 = 6;
 
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
