@@ -55,26 +55,43 @@ hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const flo
 // python_speech_features convention): y[0] = x[0], y[t] = x[t] - a x[t-1]
 // along each row (a whole clip is one row).  Elementwise, 16-B vector loads
 // of four samples plus the one before them; out of place.
+// y[0] = x[0], y[t] = x[t] - a x[t-1] per row (python_speech_features
+// sigproc.preemphasis; an optional stage, not in the reference).  Rows go
+// over blockIdx.y (no 64-bit division per element); 16-B aligned rows move
+// as float4 (four outputs per lane, the one earlier sample as a scalar load
+// that the neighbour lane's vector load has already brought into L1).
+template <bool VEC4>
 __global__ __launch_bounds__(256) void preemphasis_kernel(const float* __restrict__ x, float* __restrict__ y,
                                                           int64_t n_rows, int64_t row_len, int64_t stride,
                                                           float a) {
 #pragma clang fp contract(off)  // a rounded product, then the difference: numpy's two roundings
   const int64_t quads = (row_len + 3) / 4;
-  const int64_t total = n_rows * quads;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / quads, q = i - r * quads;
+  for (int64_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
     const float* xr = x + r * stride;
     float* yr = y + r * stride;
-    const int64_t t0 = 4 * q;
-    float prev = t0 > 0 ? xr[t0 - 1] : 0.f;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < quads;
+         q += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t t0 = 4 * q;
+      const float prev = t0 > 0 ? xr[t0 - 1] : 0.f;
+      if (VEC4 && t0 + 3 < row_len) {
+        const float4 v = *reinterpret_cast<const float4*>(xr + t0);
+        float4 o;
+        o.x = t0 == 0 ? v.x : v.x - a * prev;
+        o.y = v.y - a * v.x;
+        o.z = v.z - a * v.y;
+        o.w = v.w - a * v.z;
+        *reinterpret_cast<float4*>(yr + t0) = o;
+      } else {
+        float p = prev;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t t = t0 + k;
-      if (t < row_len) {
-        const float v = xr[t];
-        yr[t] = t == 0 ? v : v - a * prev;
-        prev = v;
+        for (int k = 0; k < 4; ++k) {
+          const int64_t t = t0 + k;
+          if (t < row_len) {
+            const float v = xr[t];
+            yr[t] = t == 0 ? v : v - a * p;
+            p = v;
+          }
+        }
       }
     }
   }
@@ -83,10 +100,19 @@ __global__ __launch_bounds__(256) void preemphasis_kernel(const float* __restric
 hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,
                               hipStream_t st) {
   if (n_rows <= 0 || row_len <= 0) return hipSuccess;
-  int64_t blocks = (n_rows * ((row_len + 3) / 4) + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(preemphasis_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, y, n_rows, row_len, stride,
-                     a);
+  const int64_t quads = (row_len + 3) / 4;
+  int64_t bx = (quads + 255) / 256;
+  if (bx > 8192) bx = 8192;
+  int64_t by = n_rows < 65535 ? n_rows : 65535;
+  while (bx * by > 65536 && bx > 1) bx = (bx + 1) / 2;  // about 16M threads in all
+  const bool vec4 = (reinterpret_cast<uintptr_t>(x) % 16 == 0) && (reinterpret_cast<uintptr_t>(y) % 16 == 0) &&
+                    (n_rows == 1 || stride % 4 == 0);
+  if (vec4)
+    hipLaunchKernelGGL(preemphasis_kernel<true>, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, st, x, y, n_rows,
+                       row_len, stride, a);
+  else
+    hipLaunchKernelGGL(preemphasis_kernel<false>, dim3((unsigned)bx, (unsigned)by), dim3(256), 0, st, x, y, n_rows,
+                       row_len, stride, a);
   return hipGetLastError();
 }
 
