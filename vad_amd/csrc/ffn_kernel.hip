@@ -332,11 +332,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 // frees their ~70 VGPRs for a third wave per SIMD while the split-f16
 // fragments stay in VGPRs (a lone wave issues scalar VALU work at about a
 // third of the rate two waves reach together: tools/micro/mfma_valu_overlap)
+#ifndef VAD_FFN_ALL_LDS
+#define VAD_FFN_ALL_LDS 1  // 13-64-64-2: fragments and slots in LDS, 4 waves per SIMD (0: 3 waves)
+#endif
 template <int KS0, int NC>
 struct WaveResidency {
-  static constexpr bool kLdsFrags = KS0 == 10 || NC > 2;
-  static constexpr bool kLdsSlots = VAD_FFN_LDS_SLOTS != 0 && !kLdsFrags;
-  static constexpr int kWavesPerSimd = KS0 == 10 ? 3 : kLdsSlots ? 3 : 2;
+  static constexpr bool kAll = VAD_FFN_ALL_LDS != 0 && KS0 == 4 && NC <= 2;
+  static constexpr bool kLdsFrags = KS0 == 10 || NC > 2 || kAll;
+  static constexpr bool kLdsSlots = (VAD_FFN_LDS_SLOTS != 0 && !kLdsFrags) || kAll;
+  static constexpr int kWavesPerSimd = kAll ? 4 : KS0 == 10 ? 3 : kLdsSlots ? 3 : 2;
 };
 // Fragments with the hi halves (and layer 0's lo halves) in VGPRs and the lo
 // halves of slots >= LO_FROM read from a workgroup-shared LDS copy
@@ -394,7 +398,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
 #define VAD_FFN_LO_ALL 1  // 1: every lo half in LDS; 0: those after layer 0 only
 #endif
   constexpr int kLoFrom = VAD_FFN_LO_ALL ? 0 : HP::S0;
-  constexpr int kLoSlots = kLdsSlots ? HP::NS - kLoFrom : 0;
+  constexpr int kLoSlots = kLdsSlots && !kLdsFrags ? HP::NS - kLoFrom : 0;
   __shared__ u4 fhlo_s[kLoSlots > 0 ? kLoSlots * 64 : 1];
   float fa[1];
   float fb[kLdsSlots ? 1 : TP::NB];
@@ -480,20 +484,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
       store_logits(net.logits, w, z, net.n_classes);
     }
   };
-  // VAD_FFN_PF tiles per trip, each with its own prefetch registers (no
-  // copies at the back edge): a tile's rows are loaded PF tiles ahead
-  float pre[VAD_FFN_PF][kWRowRegs];
+  // kPF tiles per trip (VAD_FFN_PF; 1 in the all-LDS residency, whose
+  // 128-VGPR budget a second prefetch set would spill), each with its own
+  // prefetch registers (no copies at the back edge): a tile's rows are
+  // loaded kPF tiles ahead
+  constexpr int kPF = WaveResidency<KS0, NC>::kAll ? 1 : VAD_FFN_PF;
+  float pre[kPF][kWRowRegs];
 #pragma unroll
-  for (int k = 0; k < VAD_FFN_PF; ++k) {
+  for (int k = 0; k < kPF; ++k) {
     const int64_t tk = wave_id + k * n_waves;
     load(tk < n_tiles ? tk : 0, pre[k]);
   }
-  for (int64_t t = wave_id; t < n_tiles; t += VAD_FFN_PF * n_waves) {
+  for (int64_t t = wave_id; t < n_tiles; t += kPF * n_waves) {
 #pragma unroll
-    for (int k = 0; k < VAD_FFN_PF; ++k) {
+    for (int k = 0; k < kPF; ++k) {
       const int64_t tk = t + k * n_waves;
       if (k > 0 && tk >= n_tiles) break;
-      tile_body(tk, tk + VAD_FFN_PF * n_waves, pre[k]);
+      tile_body(tk, tk + kPF * n_waves, pre[k]);
     }
   }
 }
