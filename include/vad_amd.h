@@ -290,6 +290,17 @@ int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, 
 int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
                    int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
                    float* ring, int32_t* count, uint8_t* labels, void* stream);
+/* n_hops consecutive hops of every stream in ONE kernel: exactly n_hops calls
+ * of vad_stream_hop, hop k's new samples at hop + k * hop_block_stride (row s
+ * at + s * hop_stride), its labels at labels + k * label_block_stride.  The
+ * plan tables are staged into LDS once per launch instead of once per hop;
+ * the form a hipGraph captures for many hops per replay (n_hops = 1 is
+ * vad_stream_hop).  Same refusals as vad_stream_hop, plus VAD_EINVAL for
+ * n_hops < 0 or (n_hops > 1 and label_block_stride < n_streams). */
+int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
+                    int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
+                    int32_t n_hops, int64_t hop_block_stride, float* ring, int32_t* count, uint8_t* labels,
+                    int64_t label_block_stride, void* stream);
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);

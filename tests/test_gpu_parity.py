@@ -442,6 +442,101 @@ def test_stream_batch_matches_clip_path(torch_cuda, golden, S):
             np.testing.assert_array_equal(got[:, 5:][ok], want[:, :T - 5][ok])
 
 
+@pytest.mark.parametrize("topo", [(13, 64, 64, 2), (13, 64, 64, 3)])
+def test_stream_hop_narrow_networks(torch_cuda, topo):
+    """The one-kernel hop with a network that takes only the 13 normalised
+    coefficients (layer 0 reads its inputs in fours: columns 13..15 must be
+    zeros, not D1[0..2]): labels vs the oracle on x[:, :13] of each stream's
+    features, wherever the oracle's top-2 margin exceeds 1e-3."""
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.stream import StreamBatch
+    S, T = 8, 40
+    layers = random_layers(topo, seed=11)
+    clips = [O.synth_clip(160 * (T - 1) + 401, seed=700 + s) for s in range(S)]
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    sb = StreamBatch(S, FFNClassifier(layers), kernel="hop")
+    sb.prime(torch_cuda.from_numpy(np.stack([c[:240] for c in clips])).cuda())
+    got = []
+    for t in range(T):
+        new = np.stack([c[240 + 160 * t: 400 + 160 * t] for c in clips])
+        got.append(sb.step(torch_cuda.from_numpy(new).cuda()).cpu().numpy().copy())
+    got = np.stack(got, axis=1)[:, 5:]  # (S, T-5)
+    n_ok = 0
+    for s, c in enumerate(clips):
+        x = O.analyser_features_fast(O.mfcc_batch(c, fb))[:, :13]
+        ok = O.ffn_margin(x, layers) > 1e-3
+        np.testing.assert_array_equal(got[s][ok], O.ffn_labels(x, layers)[ok])
+        n_ok += int(ok.sum())
+    assert n_ok > 0.95 * got.size
+    assert len(np.unique(got)) >= 2
+
+
+@pytest.mark.parametrize("kernel,K", [("hop", 2), ("hop", 8), ("three", 3)])
+def test_stream_hop_blocks_equal_single_hops(torch_cuda, golden, kernel, K):
+    """K hops per step (vad_stream_hops: one launch; the three-kernel form: K
+    pushes + steps), launched directly and as a captured hipGraph reading its
+    static input block in place: labels, frames, ring and counts identical to
+    K single-hop steps."""
+    import torch
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    S, nb = 24, 6
+    T = K * nb
+    clips = [O.synth_clip(160 * (T - 1) + 401, seed=800 + s) for s in range(S)]
+    carry = torch.from_numpy(np.stack([c[:240] for c in clips])).cuda()
+    hops = torch.from_numpy(np.ascontiguousarray(
+        np.stack([np.stack([c[240 + 160 * t: 400 + 160 * t] for c in clips]) for t in range(T)]))).cuda()
+    ref = StreamBatch(S, clf, kernel=kernel)
+    ref.prime(carry)
+    want = torch.stack([ref.step(hops[t]).clone() for t in range(T)])  # (T, S)
+    for graph in (False, True):
+        sb = StreamBatch(S, clf, kernel=kernel, hops_per_step=K)
+        sb.prime(carry)
+        if graph:
+            sb.capture()
+        got = []
+        for b in range(nb):
+            blk = hops[b * K:(b + 1) * K]
+            if graph:
+                sb.inputs.copy_(blk)  # the producer's write into the static block
+                got.append(sb.step_block().clone())
+            else:
+                got.append(sb.step_block(blk).clone())
+        got = torch.cat(got)
+        assert torch.equal(got, want), (graph, int((got != want).sum()))
+        assert torch.equal(sb.frames, ref.frames) and torch.equal(sb.ring, ref.ring)
+        assert torch.equal(sb.count, ref.count)
+    assert (want[:5] == 255).all() and (want[5:] != 255).all()
+
+
+def test_stream_hop_rejects_window(torch_cuda):
+    """An analysis-window plan cannot run the one-kernel hop (its table blob
+    has no window): StreamBatch refuses it, and so does the C ABI."""
+    import torch
+    from vad_amd import _lib
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.plan import MfccPlan
+    from vad_amd.stream import StreamBatch
+    clf = FFNClassifier(random_layers((39, 64, 32, 16, 3), seed=1))
+    cfg = MfccConfig(window="hamming")
+    with pytest.raises(ValueError):
+        StreamBatch(2, clf, cfg=cfg, kernel="hop")
+    StreamBatch(2, clf, cfg=cfg, kernel="three")  # the three-kernel form applies it
+    plan = MfccPlan.from_config(cfg)
+    S = 2
+    frames = torch.zeros((S, 400), device="cuda")
+    hop = torch.zeros((S, 160), device="cuda")
+    ring = torch.zeros((S, 5, 13), device="cuda")
+    count = torch.zeros((S,), dtype=torch.int32, device="cuda")
+    labels = torch.zeros((S,), dtype=torch.uint8, device="cuda")
+    rc = _lib.lib().vad_stream_hop(plan.handle, clf.plan.handle, _lib.ptr(frames), 400, 400, _lib.ptr(hop), 160,
+                                   160, S, _lib.ptr(ring), _lib.ptr(count), _lib.ptr(labels), _lib.stream_ptr())
+    assert rc == _lib.VAD_EUNSUPPORTED
+
+
 @pytest.mark.parametrize("L,H", [(400, 160), (400, 400), (600, 1), (1024, 160)])
 def test_stream_push_hop(torch_cuda, L, H):
     """vad_stream_push_hop == shift left by H and append the new samples."""

@@ -173,3 +173,25 @@ def test_optional_stages_default_off_and_oracle_restatement():
     assert y[0] == clip[0]
     np.testing.assert_allclose(y[1:], clip[1:] - np.float32(0.97) * clip[:-1], rtol=0, atol=0)
     assert not np.allclose(O.mfcc_batch(clip, fb, window=np.hamming(400)), base)
+
+
+def test_sharded_clip_rejects_segment_preemphasis():
+    """Pre-emphasis of a shard's segment would treat its first sample as the
+    clip's first (advisor finding): the sharded path refuses it after the
+    first shard and asks for whole-clip pre-emphasis instead."""
+    import torch
+    from vad_amd.config import MfccConfig
+    from vad_amd.dist import classify_clip_shard, split_clip
+
+    class _Pipe:
+        cfg = MfccConfig(preemph=0.97)
+
+        def labels(self, *a, **k):
+            raise AssertionError("not reached")
+
+    n = 160 * 999 + 401
+    sh = split_clip(n, 1, 2)
+    assert sh.sample_lo > 0
+    seg = torch.zeros((sh.sample_hi - sh.sample_lo,))
+    with pytest.raises(ValueError):
+        classify_clip_shard(_Pipe(), seg, sh)

@@ -70,6 +70,8 @@ SIGNATURES = {
     "vad_stream_push_hop": (c_int, [c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp]),
     "vad_stream_hop": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp,
                                c_vp]),
+    "vad_stream_hops": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_i64, c_i32, c_i64, c_i32, c_i64, c_vp,
+                                c_vp, c_vp, c_i64, c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                 c_vp]),
     "vad_rccl_available": (c_int, []),

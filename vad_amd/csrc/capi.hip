@@ -697,19 +697,30 @@ int vad_stream_push_hop(float* frames, int64_t frame_stride, int32_t frame_len, 
                                  (hipStream_t)stream);
 }
 
-int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
-                   int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
-                   float* ring, int32_t* count, uint8_t* labels, void* stream) {
-  if (!plan || !ffn || n_streams < 0 || frame_len <= 0 || frame_len > 1024 || hop_len <= 0 ||
+int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
+                    int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
+                    int32_t n_hops, int64_t hop_block_stride, float* ring, int32_t* count, uint8_t* labels,
+                    int64_t label_block_stride, void* stream) {
+  if (!plan || !ffn || n_streams < 0 || n_hops < 0 || frame_len <= 0 || frame_len > 1024 || hop_len <= 0 ||
       hop_len > frame_len || frame_stride < frame_len || hop_stride < hop_len)
     return VAD_EINVAL;
-  if (n_streams == 0) return VAD_OK;
+  if (n_hops > 1 && label_block_stride < n_streams) return VAD_EINVAL;  // label rows of two hops would overlap
+  if (n_streams == 0 || n_hops == 0) return VAD_OK;
   if (!frames || !hop || !ring || !count || !labels) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
   if (plan->generic()) return VAD_EUNSUPPORTED;  // its FFT is the 256-point Stockham of fft_n = 512
+  if (plan->spec == kSpecWindow) return VAD_EUNSUPPORTED;  // its table blob carries no analysis window
   return (int)launch_stream_hop(plan->dev, plan->hop_blob, plan->hop_blob_n, plan->host.n_filters, plan->n_taps,
                                 ffn->net, frames, frame_stride, frame_len, hop, hop_stride, hop_len,
-                                n_streams, plan->host.mfcc_n, ring, count, labels, (hipStream_t)stream);
+                                n_streams, plan->host.mfcc_n, ring, count, labels, n_hops, hop_block_stride,
+                                label_block_stride, (hipStream_t)stream);
+}
+
+int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
+                   int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
+                   float* ring, int32_t* count, uint8_t* labels, void* stream) {
+  return vad_stream_hops(plan, ffn, frames, frame_stride, frame_len, hop, hop_stride, hop_len, n_streams, 1, 0,
+                         ring, count, labels, 0, stream);
 }
 
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
                                                           const float* __restrict__ hop, int64_t hstride,
                                                           int hlen, int64_t n_streams, int mfcc_n,
                                                           float* __restrict__ ring, int* __restrict__ count,
-                                                          uint8_t* __restrict__ labels) {
+                                                          uint8_t* __restrict__ labels, int n_hops,
+                                                          int64_t hop_kstride, int64_t lab_kstride) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   const int waves = blockDim.x >> 6;
   // -- stage the plans' tables (the MFCC plan's hop blob, then the FFN
@@ -224,201 +225,239 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int64_t s = (int64_t)blockIdx.x * waves + wv;
-  // -- frame: shift by the hop, append the new samples (stream_push_kernel);
-  // issued before the barrier, so their latency overlaps the staging
-  float* row = frames + (s < n_streams ? s : 0) * fstride;
-  const float* hs = hop + (s < n_streams ? s : 0) * hstride;
+  const int64_t sc = s < n_streams ? s : 0;
+  // -- the stream's state, requested before the barrier so its latency
+  // overlaps the staging: the frame as it stands (registers, sample
+  // t = lane + 64 i), the first hop's new samples at the positions they take
+  // in the advanced frame, the frame count and the MFCC ring
+  float* row = frames + sc * fstride;
   const int keep = len - hlen;
-  float v[16];
+  float v[16], hn[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int t = lane + 64 * i;
-    v[i] = t < keep ? row[t + hlen] : (t < len ? hs[t - keep] : 0.f);
+    v[i] = t < len ? row[t] : 0.f;
+    hn[i] = (t >= keep && t < len) ? hop[sc * hstride + (t - keep)] : 0.f;
   }
-  // the stream's frame count and MFCC ring, requested now too (the window
-  // needs them only after the FFT)
-  const int64_t sc = s < n_streams ? s : 0;
-  const int c = count[sc];
+  int c = count[sc];
   float* rs = ring + sc * 5 * mfcc_n;
   float rv[5];
 #pragma unroll
   for (int d = 0; d < 5; ++d) rv[d] = lane < mfcc_n ? rs[d * mfcc_n + lane] : 0.f;
   __syncthreads();
   if (s >= n_streams) return;  // wave-uniform; no barrier below
-  if (VAD_HOP_DIAG == 1) {
-    if (lane == 0) labels[s] = (uint8_t)v[0];
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int t = lane + 64 * i;
-    if (t < len) row[t] = v[i];
-  }
   float* scr = hsm + wv * kHopWaveFloats;
   float2* z0 = reinterpret_cast<float2*>(scr);
   float2* z1 = reinterpret_cast<float2*>(scr + kHopZ);
   float* lmr = scr + 2 * kHopZ;
   float* act_a = lmr + kMaxFilters;
   float* act_b = act_a + 64;
-  // samples of the FFT (np.fft.fft(x, 512): zero-pad / truncate, mfcc.py:61)
+  float* fb = scr;  // the frame shift goes through the FFT buffers (2 kHopZ >= 1024 floats)
   const int used = len < kFftN ? len : kFftN;
-  float* xs = reinterpret_cast<float*>(z1);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int t = lane + 64 * i;  // sample t = component t & 1 of complex t / 2
-    xs[2 * zp(t >> 1) + (t & 1)] = t < used ? v[i] : 0.f;
-  }
-  // LDS is in order within a wave; these keep the compiler from moving
-  // accesses of one phase (other lanes' data, other element types) across
-  // the next
-  asm volatile("" ::: "memory");
 
-  // -- 256-point complex FFT, Stockham radix-4
-  float2* src = z1;
-  float2* dst = z0;
+  // K hops of this stream back to back: the same computation per hop as K
+  // launches of one hop (state carried in registers), the tables staged once
+  for (int k = 0; k < n_hops; ++k) {
+    // -- frame: shift by the hop (through LDS: sample t + hlen belongs to
+    // another lane), append the new samples (stream_push_kernel)
 #pragma unroll
-  for (int st = 0; st < 4; ++st) {
-    const int ns = 1 << (2 * st);  // 1, 4, 16, 64
-    const int k = lane & (ns - 1);
-    float2 a0 = src[zp(lane)], a1 = src[zp(lane + 64)], a2 = src[zp(lane + 128)], a3 = src[zp(lane + 192)];
-    if (st > 0) {
-      const int m = k * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
-      a1 = cmulf(a1, w256(T.tw, m));
-      a2 = cmulf(a2, w256(T.tw, 2 * m));
-      a3 = cmulf(a3, w256(T.tw, 3 * m));
+    for (int i = 0; i < 16; ++i) {
+      const int t = lane + 64 * i;
+      if (t < len) fb[t] = v[i];
     }
-    const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
-    const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
-    const int o = (lane >> (2 * st)) * (4 * ns) + k;
-    dst[zp(o)] = make_float2(b0.x + b2.x, b0.y + b2.y);
-    dst[zp(o + ns)] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
-    dst[zp(o + 2 * ns)] = make_float2(b0.x - b2.x, b0.y - b2.y);
-    dst[zp(o + 3 * ns)] = make_float2(b1.x - b3.y, b1.y + b3.x);  // b1 + i b3
-    float2* t = src;
-    src = dst;
-    dst = t;
     asm volatile("" ::: "memory");
-  }
-  if (VAD_HOP_DIAG == 2) {
-    if (lane == 0) labels[s] = (uint8_t)src[3].x;
-    return;
-  }
-  // -- real-FFT split: 2X[k] = S - i W512^k D, S = Z[k] + conj(Z[-k]),
-  // D = Z[k] - conj(Z[-k]); |2X|^2 into the free buffer
-  float* pw = reinterpret_cast<float*>(dst);
-  float pk[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int k = lane + 64 * q;
-    const float2 zk = src[zp(k)], zn = src[zp((256 - k) & 255)];
-    const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
-    const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
-    const float2 Tw = cmulf(D, T.tw[k]);
-    const float u = S.x + Tw.y, vv = S.y - Tw.x;
-    pk[q] = fmaf(u, u, vv * vv);
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) pw[lane + 64 * q] = pk[q];
-  asm volatile("" ::: "memory");
-  // -- mel + log10 (lane m), lifter x DCT (lane c)
-  if (lane < nf) {
-    const int lo = T.f_lo[lane], n = T.f_len[lane];
-    const float* wt = T.taps + T.f_off[lane];
-    // unrolled: the LDS reads of a batch are in flight together (a rolled
-    // loop waits one LDS round trip per tap)
-    float e = 0.f;
-#pragma unroll 8
-    for (int t = 0; t < n; ++t) e = fmaf(wt[t], pw[lo + t], e);
-    lmr[lane] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
-  }
-  asm volatile("" ::: "memory");
-  float mf = 0.f;
-  if (lane < mfcc_n) {
-    const float* d = T.dct + lane * nf;
-#pragma unroll 8
-    for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
-  }
-
-  if (VAD_HOP_DIAG == 3) {
-    if (lane == 0) labels[s] = (uint8_t)mf;
-    return;
-  }
-  // -- window of the five previous frames, then push the new row
-  const bool have = c >= 5;
-  act_a[lane] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
-  asm volatile("" ::: "memory");
-  if (lane < mfcc_n) {
-    if (have) {
-      // slot (c + d) % 5, d = 0..4: the ring in arrival order, oldest first
-      float r[5];
-#pragma unroll
-      for (int d = 0; d < 5; ++d) {
-        const int q = (c + d) % 5;
-        r[d] = q == 0 ? rv[0] : q == 1 ? rv[1] : q == 2 ? rv[2] : q == 3 ? rv[3] : rv[4];
-      }
-      const Feat3 ft = feature_triple(r[0], r[1], r[2], r[3], r[4], VAD_FEAT_ANALYSER);
-      act_a[lane] = ft.mn;
-      act_a[mfcc_n + lane] = ft.d1;
-      act_a[2 * mfcc_n + lane] = ft.d2;
+    for (int i = 0; i < 16; ++i) {
+      const int t = lane + 64 * i;
+      v[i] = t < keep ? fb[t + hlen] : hn[i];
     }
-    rs[(c % 5) * mfcc_n + lane] = mf;
-  }
-  asm volatile("" ::: "memory");
-  uint8_t label = 255;
-  if (have && VAD_HOP_DIAG != 4) {
-    // -- FFN: exact f32, lane o of each layer
-    float* hin = act_a;
-    float* hout = act_b;
-    const int nl = net.n_layers;
-    for (int l = 0; l < nl; ++l) {
-      const int din = net.dims[l], dout = net.dims[l + 1];
-#ifndef VAD_HOP_VEC
-#define VAD_HOP_VEC 1
-#endif
-      // four inputs per step (one ds_read_b128 broadcast), four partial
-      // sums; inputs past din are zero and the weight rows past W_l read
-      // the next finite values of the block (zero-padded at its end)
-      const float* W = T.w + net.woff[l];
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-      if (lane < dout) {
-        if (VAD_HOP_VEC) {
-          const float4* h4 = reinterpret_cast<const float4*>(hin);
-#pragma unroll 4
-          for (int k = 0; k < din; k += 4) {
-            const float4 h = h4[k >> 2];
-            a0 = fmaf(W[k * dout + lane], h.x, a0);
-            a1 = fmaf(W[(k + 1) * dout + lane], h.y, a1);
-            a2 = fmaf(W[(k + 2) * dout + lane], h.z, a2);
-            a3 = fmaf(W[(k + 3) * dout + lane], h.w, a3);
-          }
-        } else {
-#pragma unroll 8
-          for (int k = 0; k < din; ++k) a0 = fmaf(W[k * dout + lane], hin[k], a0);
-        }
+    asm volatile("" ::: "memory");
+    if (k + 1 < n_hops) {  // the next hop's samples, in flight during this one
+      const float* hs = hop + (int64_t)(k + 1) * hop_kstride + s * hstride;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int t = lane + 64 * i;
+        hn[i] = (t >= keep && t < len) ? hs[t - keep] : 0.f;
       }
-      const float acc = T.w[net.boff[l] + (lane < dout ? lane : 0)] + ((a0 + a1) + (a2 + a3));
-      hout[lane] = lane < dout ? (l + 1 < nl ? relu_nan(acc) : acc) : 0.f;
-      float* t = hin;
-      hin = hout;
-      hout = t;
+    }
+    uint8_t* lab_k = labels + (int64_t)k * lab_kstride;
+    if (VAD_HOP_DIAG == 1) {
+      if (lane == 0) lab_k[s] = (uint8_t)v[0];
+      continue;
+    }
+    // samples of the FFT (np.fft.fft(x, 512): zero-pad / truncate, mfcc.py:61)
+    float* xs = reinterpret_cast<float*>(z1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = lane + 64 * i;  // sample t = component t & 1 of complex t / 2
+      xs[2 * zp(t >> 1) + (t & 1)] = t < used ? v[i] : 0.f;
+    }
+    // LDS is in order within a wave; these keep the compiler from moving
+    // accesses of one phase (other lanes' data, other element types) across
+    // the next
+    asm volatile("" ::: "memory");
+
+    // -- 256-point complex FFT, Stockham radix-4
+    float2* src = z1;
+    float2* dst = z0;
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const int ns = 1 << (2 * st);  // 1, 4, 16, 64
+      const int kk = lane & (ns - 1);
+      float2 a0 = src[zp(lane)], a1 = src[zp(lane + 64)], a2 = src[zp(lane + 128)], a3 = src[zp(lane + 192)];
+      if (st > 0) {
+        const int m = kk * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
+        a1 = cmulf(a1, w256(T.tw, m));
+        a2 = cmulf(a2, w256(T.tw, 2 * m));
+        a3 = cmulf(a3, w256(T.tw, 3 * m));
+      }
+      const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
+      const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
+      const int o = (lane >> (2 * st)) * (4 * ns) + kk;
+      dst[zp(o)] = make_float2(b0.x + b2.x, b0.y + b2.y);
+      dst[zp(o + ns)] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
+      dst[zp(o + 2 * ns)] = make_float2(b0.x - b2.x, b0.y - b2.y);
+      dst[zp(o + 3 * ns)] = make_float2(b1.x - b3.y, b1.y + b3.x);  // b1 + i b3
+      float2* t = src;
+      src = dst;
+      dst = t;
       asm volatile("" ::: "memory");
     }
-    const f32x4 zl = {hin[0], hin[1 < net.n_classes ? 1 : 0], hin[2 < net.n_classes ? 2 : 0],
-                      hin[3 < net.n_classes ? 3 : 0]};
-    label = (uint8_t)argmax_classes(zl, net.n_classes);
+    if (VAD_HOP_DIAG == 2) {
+      if (lane == 0) lab_k[s] = (uint8_t)src[3].x;
+      continue;
+    }
+    // -- real-FFT split: 2X[k] = S - i W512^k D, S = Z[k] + conj(Z[-k]),
+    // D = Z[k] - conj(Z[-k]); |2X|^2 into the free buffer
+    float* pw = reinterpret_cast<float*>(dst);
+    float pk[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int kb = lane + 64 * q;
+      const float2 zk = src[zp(kb)], zn = src[zp((256 - kb) & 255)];
+      const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
+      const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
+      const float2 Tw = cmulf(D, T.tw[kb]);
+      const float u = S.x + Tw.y, vv = S.y - Tw.x;
+      pk[q] = fmaf(u, u, vv * vv);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) pw[lane + 64 * q] = pk[q];
+    asm volatile("" ::: "memory");
+    // -- mel + log10 (lane m), lifter x DCT (lane c)
+    if (lane < nf) {
+      const int lo = T.f_lo[lane], n = T.f_len[lane];
+      const float* wt = T.taps + T.f_off[lane];
+      // unrolled: the LDS reads of a batch are in flight together (a rolled
+      // loop waits one LDS round trip per tap)
+      float e = 0.f;
+#pragma unroll 8
+      for (int t = 0; t < n; ++t) e = fmaf(wt[t], pw[lo + t], e);
+      lmr[lane] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
+    }
+    asm volatile("" ::: "memory");
+    float mf = 0.f;
+    if (lane < mfcc_n) {
+      const float* d = T.dct + lane * nf;
+#pragma unroll 8
+      for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
+    }
+
+    if (VAD_HOP_DIAG == 3) {
+      if (lane == 0) lab_k[s] = (uint8_t)mf;
+      continue;
+    }
+    // -- window of the five previous frames, then push the new row
+    const bool have = c >= 5;
+    act_a[lane] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
+    asm volatile("" ::: "memory");
+    if (lane < mfcc_n) {
+      if (have) {
+        // slot (c + d) % 5, d = 0..4: the ring in arrival order, oldest first
+        float r[5];
+#pragma unroll
+        for (int d = 0; d < 5; ++d) {
+          const int q = (c + d) % 5;
+          r[d] = q == 0 ? rv[0] : q == 1 ? rv[1] : q == 2 ? rv[2] : q == 3 ? rv[3] : rv[4];
+        }
+        const Feat3 ft = feature_triple(r[0], r[1], r[2], r[3], r[4], VAD_FEAT_ANALYSER);
+        act_a[lane] = ft.mn;
+        act_a[mfcc_n + lane] = ft.d1;
+        act_a[2 * mfcc_n + lane] = ft.d2;
+      }
+      const int q = c % 5;  // the push (ring slot of the oldest row)
+#pragma unroll
+      for (int d = 0; d < 5; ++d) rv[d] = q == d ? mf : rv[d];
+    }
+    asm volatile("" ::: "memory");
+    {
+      // layer 0 reads its inputs in fours: a network narrower than the feature
+      // triple (13-64-64-N takes the 13 normalised coefficients) must see zeros,
+      // not the delta columns, in the rest of its last block (stored after the
+      // features: LDS is in order per wave)
+      const int din0 = net.dims[0];
+      if (lane >= din0 && lane < ((din0 + 3) & ~3)) act_a[lane] = 0.f;
+    }
+    asm volatile("" ::: "memory");
+    uint8_t label = 255;
+    if (have && VAD_HOP_DIAG != 4) {
+      // -- FFN: exact f32, lane o of each layer
+      float* hin = act_a;
+      float* hout = act_b;
+      const int nl = net.n_layers;
+      for (int l = 0; l < nl; ++l) {
+        const int din = net.dims[l], dout = net.dims[l + 1];
+        // four inputs per step (one ds_read_b128 broadcast), four partial
+        // sums; inputs past din are zero and the weight rows past W_l read
+        // the next finite values of the block (zero-padded at its end)
+        const float* W = T.w + net.woff[l];
+        float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+        if (lane < dout) {
+          const float4* h4 = reinterpret_cast<const float4*>(hin);
+#pragma unroll 4
+          for (int kq = 0; kq < din; kq += 4) {
+            const float4 h = h4[kq >> 2];
+            a0 = fmaf(W[kq * dout + lane], h.x, a0);
+            a1 = fmaf(W[(kq + 1) * dout + lane], h.y, a1);
+            a2 = fmaf(W[(kq + 2) * dout + lane], h.z, a2);
+            a3 = fmaf(W[(kq + 3) * dout + lane], h.w, a3);
+          }
+        }
+        const float acc = T.w[net.boff[l] + (lane < dout ? lane : 0)] + ((a0 + a1) + (a2 + a3));
+        hout[lane] = lane < dout ? (l + 1 < nl ? relu_nan(acc) : acc) : 0.f;
+        float* t = hin;
+        hin = hout;
+        hout = t;
+        asm volatile("" ::: "memory");
+      }
+      const f32x4 zl = {hin[0], hin[1 < net.n_classes ? 1 : 0], hin[2 < net.n_classes ? 2 : 0],
+                        hin[3 < net.n_classes ? 3 : 0]};
+      label = (uint8_t)argmax_classes(zl, net.n_classes);
+    }
+    if (lane == 0) lab_k[s] = label;
+    c = (c + 1 >= 10) ? c + 1 - 5 : c + 1;
+    asm volatile("" ::: "memory");
   }
-  if (lane == 0) {
-    labels[s] = label;
-    count[s] = (c + 1 >= 10) ? c + 1 - 5 : c + 1;
+  // -- the stream's state back: frame, ring, count
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int t = lane + 64 * i;
+    if (t < len) row[t] = v[i];
   }
+  if (lane < mfcc_n) {
+#pragma unroll
+    for (int d = 0; d < 5; ++d) rs[d * mfcc_n + lane] = rv[d];
+  }
+  if (lane == 0) count[s] = c;
 }
 
 hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n, int nf, int n_taps,
                              const FfnDev& net, float* frames, int64_t fstride, int len, const float* hop,
                              int64_t hstride, int hlen, int64_t n_streams, int mfcc_n, float* ring, int* count,
-                             uint8_t* labels, hipStream_t st) {
+                             uint8_t* labels, int n_hops, int64_t hop_kstride, int64_t lab_kstride,
+                             hipStream_t st) {
   (void)plan;
-  if (n_streams <= 0) return hipSuccess;
+  if (n_streams <= 0 || n_hops <= 0) return hipSuccess;
   const size_t tables = (size_t)(blob_n + net.wraw_n) * sizeof(float);
   // streams per block: at least VAD_HOP_MIN_WAVES (one wave per SIMD), then
   // spread over every CU (each block stages the ~26 KB of tables from L2
@@ -446,7 +485,8 @@ hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n,
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)((n_streams + waves - 1) / waves));
   hipLaunchKernelGGL(stream_hop_kernel, grid, dim3(64 * waves), smem, st, blob, blob_n, nf, n_taps, net, frames,
-                     fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels);
+                     fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels, n_hops, hop_kstride,
+                     lab_kstride);
   return hipGetLastError();
 }
 

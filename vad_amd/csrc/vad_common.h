@@ -109,7 +109,8 @@ hipError_t launch_stream_ffn(const FfnDev& net, const float* newrow, float* ring
 hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n, int nf, int n_taps,
                              const FfnDev& net, float* frames, int64_t fstride, int len,
                              const float* hop, int64_t hstride, int hlen, int64_t n_streams, int mfcc_n,
-                             float* ring, int* count, uint8_t* labels, hipStream_t st);
+                             float* ring, int* count, uint8_t* labels, int n_hops, int64_t hop_kstride,
+                             int64_t lab_kstride, hipStream_t st);
 hipError_t launch_stream_push(float* frames, int64_t fstride, int len, const float* hop, int64_t hstride,
                               int hlen, int64_t n_streams, hipStream_t st);
 hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t row_len, int64_t stride, float a,

@@ -71,6 +71,11 @@ def classify_clip_shard(pipe, audio_segment, shard: ClipShard, out=None, stream=
     """Labels of this rank's windows from its (already sliced, device) segment."""
     if shard.n_windows == 0:
         return torch.empty((0,), dtype=torch.uint8, device=audio_segment.device)
+    if getattr(pipe.cfg, "preemph", None) is not None and shard.sample_lo > 0:
+        # the segment's first sample would be pre-emphasised as if it began
+        # the clip: apply vad_amd.preemphasis to the whole clip, then shard
+        # it with a pipeline whose cfg.preemph is None
+        raise ValueError("pre-emphasis must run on the whole clip before sharding")
     lab = pipe.labels(audio_segment, out=out, stream=stream)
     if lab.numel() != shard.n_windows:
         raise ValueError(f"segment of {audio_segment.numel()} samples gives {lab.numel()} windows, "
@@ -201,6 +206,8 @@ class RcclComm:
         if self.rank == root and (recv is None or recv.dtype != torch.uint8
                                   or recv.numel() != self.world * send.numel()):
             raise ValueError("recv must hold world * n uint8 on the root")
+        if self.rank == root and (not recv.is_cuda or not recv.is_contiguous() or recv.device != send.device):
+            raise TypeError("recv must be a contiguous CUDA tensor on the send tensor's device")
         _lib.check(_lib.lib().vad_rccl_gather_u8(self._h, _lib.ptr(send), _lib.ptr(recv), send.numel(), int(root),
                                                  _lib.stream_ptr(stream)), "vad_rccl_gather_u8")
         return recv

@@ -246,6 +246,11 @@ def preemphasis(x, coeff, out=None, stream=None):
     reference."""
     _require_cuda_tensor(x, "x")
     rows, n = (1, x.numel()) if x.dim() == 1 else tuple(x.shape)
+    if out is None and stream is not None:
+        # allocated on the stream that writes (and, in VadPipeline, reads) it:
+        # the caching allocator may not hand it to other streams' work early
+        with torch.cuda.stream(stream):
+            out = torch.empty(tuple(x.shape), dtype=torch.float32, device=x.device)
     out = _out(out, tuple(x.shape), torch.float32, x.device)
     check(lib().vad_preemphasis_f32(ptr(x), ptr(out), rows, n, n, ctypes.c_float(coeff), stream_ptr(stream)),
           "vad_preemphasis_f32")

@@ -14,6 +14,15 @@ step.  Two forms of a step, identical semantics:
 labels[s] after a step is the class of stream s's window centred three steps
 earlier, or 255 during each stream's first five steps (feed_frame returns
 None for its first five calls, :48-50).
+
+Blocks of hops: with hops_per_step=K a step advances every stream by K hops
+(step_block), K x 10 ms of audio per stream, whose new samples sit in the
+static input block ``inputs`` (K, S, hop) and whose labels land in
+``label_block`` (K, S).  kernel="hop" runs the K hops in ONE launch
+(vad_stream_hops: the plan tables staged once, the stream state carried in
+registers from hop to hop); capture() records one block into a hipGraph that
+reads ``inputs`` in place, so a producer that writes the next block there
+(e.g. an H2D copy of the audio devices' buffers) replays with no copy at all.
 """
 from __future__ import annotations
 
@@ -29,7 +38,8 @@ from .plan import MfccPlan
 
 class StreamBatch:
 
-    def __init__(self, n_streams, ffn, cfg: MfccConfig = MfccConfig(), device=None, kernel="hop"):
+    def __init__(self, n_streams, ffn, cfg: MfccConfig = MfccConfig(), device=None, kernel="hop",
+                 hops_per_step=1):
         if not isinstance(ffn, FFNClassifier):
             ffn = FFNClassifier(ffn)
         if cfg.preemph is not None:
@@ -37,16 +47,25 @@ class StreamBatch:
         dev = torch.device("cuda", torch.cuda.current_device()) if device is None else device
         if kernel not in ("hop", "three"):
             raise ValueError("kernel must be 'hop' or 'three'")
+        if kernel == "hop" and cfg.window is not None:
+            raise ValueError("the one-kernel hop has no analysis window; use kernel='three'")
         self.cfg, self.ffn, self.n, self.kernel = cfg, ffn, int(n_streams), kernel
         self.plan = MfccPlan.from_config(cfg)
         S, L, H, C = self.n, cfg.frame_size, cfg.hop, cfg.n_mfcc
         if not 0 < H <= L:
             raise ValueError("hop must be in (0, frame_size]")
+        K = int(hops_per_step)
+        if K < 1:
+            raise ValueError("hops_per_step must be >= 1")
+        self.K = K
         self.frames = torch.zeros((S, L), dtype=torch.float32, device=dev)
-        self.hop_in = torch.zeros((S, H), dtype=torch.float32, device=dev)   # static graph input
+        # static graph inputs / outputs: K hops of new samples, K label rows
+        self.inputs = torch.zeros((K, S, H), dtype=torch.float32, device=dev)
+        self.hop_in = self.inputs[0]
         self.ring = torch.zeros((S, 5, C), dtype=torch.float32, device=dev)
         self.count = torch.zeros((S,), dtype=torch.int32, device=dev)
-        self.labels = torch.full((S,), 255, dtype=torch.uint8, device=dev)
+        self.label_block = torch.full((K, S), 255, dtype=torch.uint8, device=dev)
+        self.labels = self.label_block[K - 1]
         self.scratch = torch.zeros((S, C), dtype=torch.float32, device=dev)
         self.graph = None
 
@@ -59,36 +78,55 @@ class StreamBatch:
         self.frames.zero_()
         self.ring.zero_()
         self.count.zero_()
-        self.labels.fill_(255)
+        self.label_block.fill_(255)
 
-    def _hop_call(self, h):
-        """vad_stream_hop with the per-batch arguments prepared once (the
-        Python side of a hop is a few microseconds of ctypes marshalling)."""
+    def _hop_call(self, h, n_hops=1, labels=None):
+        """vad_stream_hops with the per-batch arguments prepared once (the
+        Python side of a launch is a few microseconds of ctypes marshalling)."""
         if getattr(self, "_hop_args", None) is None:
             L, H = self.cfg.frame_size, self.cfg.hop
-            self._hop_fn = _lib.lib().vad_stream_hop
+            self._hop_fn = _lib.lib().vad_stream_hops
             self._hop_args = (self.plan.handle, self.ffn.plan.handle, _lib.ptr(self.frames), L, L)
-            self._hop_tail = (H, self.n, _lib.ptr(self.ring), _lib.ptr(self.count), _lib.ptr(self.labels))
-        rc = self._hop_fn(*self._hop_args, ctypes.c_void_p(h.data_ptr()), h.stride(0), *self._hop_tail,
+        H = self.cfg.hop
+        lab = self.labels if labels is None else labels
+        rc = self._hop_fn(*self._hop_args, ctypes.c_void_p(h.data_ptr()), h.stride(-2), H, self.n, n_hops,
+                          h.stride(0) if h.dim() == 3 else 0, _lib.ptr(self.ring), _lib.ptr(self.count),
+                          ctypes.c_void_p(lab.data_ptr()), lab.stride(0) if lab.dim() == 2 else 0,
                           _lib.stream_ptr())
         if rc:
-            _lib.check(rc, "vad_stream_hop")
+            _lib.check(rc, "vad_stream_hops")
 
-    def _body(self, hop=None):
+    def _three(self, h, labels):
         L, H = self.cfg.frame_size, self.cfg.hop
         lib = _lib.lib()
-        if self.kernel == "hop":
-            self._hop_call(self.hop_in if hop is None else hop)
-            return
-        _lib.check(lib.vad_stream_push_hop(_lib.ptr(self.frames), L, L, _lib.ptr(self.hop_in), H, H,
-                                           self.n, _lib.stream_ptr()), "vad_stream_push_hop")
+        _lib.check(lib.vad_stream_push_hop(_lib.ptr(self.frames), L, L, ctypes.c_void_p(h.data_ptr()), h.stride(0),
+                                           H, self.n, _lib.stream_ptr()), "vad_stream_push_hop")
         _lib.check(lib.vad_stream_step(
             self.plan.handle, self.ffn.plan.handle, _lib.ptr(self.frames), L, L, self.n,
-            _lib.ptr(self.ring), _lib.ptr(self.count), _lib.ptr(self.labels),
+            _lib.ptr(self.ring), _lib.ptr(self.count), ctypes.c_void_p(labels.data_ptr()),
             _lib.ptr(self.scratch), _lib.stream_ptr()), "vad_stream_step")
 
+    def _body(self, hop=None):
+        """One hop (K = 1) from `hop` or the static input."""
+        h = self.hop_in if hop is None else hop
+        if self.kernel == "hop":
+            self._hop_call(h)
+        else:
+            self._three(h, self.labels)
+
+    def _block_body(self):
+        """K hops from the static input block into label_block."""
+        if self.kernel == "hop":
+            self._hop_call(self.inputs, self.K, self.label_block)
+        else:
+            for k in range(self.K):
+                self._three(self.inputs[k], self.label_block[k])
+
     def step(self, new_samples=None):
-        """Advance every stream by one hop (new_samples: (S, hop) device fp32)."""
+        """Advance every stream by one hop (new_samples: (S, hop) device fp32;
+        None: the hop already written into ``hop_in``).  hops_per_step == 1."""
+        if self.K != 1:
+            raise ValueError("this batch advances hops_per_step hops at a time: use step_block")
         if new_samples is not None and (new_samples.shape != self.hop_in.shape
                                         or new_samples.dtype != torch.float32 or not new_samples.is_cuda):
             raise ValueError(f"new_samples must be a CUDA float32 tensor of shape {tuple(self.hop_in.shape)}")
@@ -104,19 +142,39 @@ class StreamBatch:
             self._body()
         return self.labels
 
+    def step_block(self, new_samples=None):
+        """Advance every stream by K = hops_per_step hops; new_samples: (K, S,
+        hop) device fp32, or None when the block was written into ``inputs``
+        (the graph's static input: no copy).  Returns label_block (K, S)."""
+        if new_samples is not None:
+            if new_samples.shape != self.inputs.shape or new_samples.dtype != torch.float32 \
+                    or not new_samples.is_cuda:
+                raise ValueError(f"new_samples must be a CUDA float32 tensor of shape {tuple(self.inputs.shape)}")
+            if self.graph is None and self.kernel == "hop" and new_samples.stride(2) == 1:
+                self._hop_call(new_samples, self.K, self.label_block)  # read in place
+                return self.label_block
+            self.inputs.copy_(new_samples)
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._block_body()
+        return self.label_block
+
     def capture(self):
-        """Capture one step into a hipGraph (torch.cuda.CUDAGraph); step() replays it."""
+        """Capture one step (K hops) into a hipGraph (torch.cuda.CUDAGraph);
+        step() / step_block() replay it, reading the static ``inputs``."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        saved = (self.frames.clone(), self.ring.clone(), self.count.clone(), self.labels.clone())
+        saved = (self.frames.clone(), self.ring.clone(), self.count.clone(), self.label_block.clone())
+        body = self._body if self.K == 1 else self._block_body
         with torch.cuda.stream(s):
-            self._body()  # warm-up (first launch sets kernel attributes)
+            body()  # warm-up (first launch sets kernel attributes)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         self.frames.copy_(saved[0]); self.ring.copy_(saved[1])
-        self.count.copy_(saved[2]); self.labels.copy_(saved[3])
+        self.count.copy_(saved[2]); self.label_block.copy_(saved[3])
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._body()
+            body()
         self.graph = g
         return g
