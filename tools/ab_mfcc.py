@@ -1,4 +1,4 @@
-"""A/B of MFCC kernel builds on one box: python tools/ab_mfcc.py LIB_A LIB_B [rounds]
+"""A/B of MFCC kernel builds on one box: python tools/ab_mfcc.py LIB_A LIB_B [LIB_C ...] [rounds]
 Alternates the two libraries (fresh processes) and prints per-launch us for
 C3 (1M frames) and C2 (100k, 6 rotated clips), fp32 input (int16 PCM with AB_I16=1)."""
 import json
@@ -35,8 +35,9 @@ c2 = t(c2f)
 print(json.dumps({"c3_us": c3, "c2_us": c2}))
 '''
 
-libs = sys.argv[1:3]
-rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+args = sys.argv[1:]
+rounds = int(args.pop()) if args and args[-1].isdigit() else 3
+libs = args
 res = {l: [] for l in libs}
 for r in range(rounds):
     for l in libs:

@@ -26,7 +26,8 @@ CONFIGS = [
     ("Mel26", 300, 8000, 26, 16000, 13, 22),   # config.py:20-27, sklearn_analyser.py:21
     ("Mel40", 300, 8000, 40, 16000, 13, 22),   # BASELINE.json config 2
 ]
-WAVES = 8          # phase-2a filter bands (one per wave)
+WAVES = 8          # phase-2a filter bands (one per wave) of mfcc_kernel
+WAVES12 = 12       # phase-2a filter bands of mfcc3_kernel (12 waves, each one band of two frame sets)
 DCT_GROUPS = 4     # phase-2b coefficient groups c = g, g+4, ... (waves 0..3)
 
 
@@ -60,6 +61,21 @@ def dct_matrix(nf, nc, L):
     return d.astype(np.float32)
 
 
+def bands(lens, waves):
+    """Contiguous filter bands balanced by cost (taps + (==0 -> eps) + log10)."""
+    nf = len(lens)
+    cost = [lens[m] + 8 for m in range(nf)]
+    total = sum(cost)
+    band, acc, m = [0], 0, 0
+    for w in range(waves):
+        target = total * (w + 1) / waves
+        while m < nf and (acc + cost[m] / 2 <= target or w == waves - 1):
+            acc += cost[m]
+            m += 1
+        band.append(m)
+    return band
+
+
 def fhex(x):
     return float(np.float32(x)).hex() + "f"
 
@@ -77,15 +93,7 @@ def emit(name, lo, hi, nf, sr, nc, L):
     dense = np.zeros((nf, 256), np.float32)
     for m in range(nf):
         dense[m, los[m]:los[m] + lens[m]] = taps[m]
-    cost = [lens[m] + 8 for m in range(nf)]  # taps + (==0 -> eps) + log10
-    total = sum(cost)
-    band, acc, m = [0], 0, 0
-    for w in range(WAVES):
-        target = total * (w + 1) / WAVES
-        while m < nf and (acc + cost[m] / 2 <= target or w == WAVES - 1):
-            acc += cost[m]
-            m += 1
-        band.append(m)
+    band = bands(lens, WAVES)
     d = dct_matrix(nf, nc, L)
     lines = [f"struct {name} {{",
              f"  static constexpr int NF = {nf};",
@@ -118,12 +126,18 @@ def emit_code(name, info):
     DCT term (VOP2 literal: no SGPR, nothing for the compiler to hoist out of
     the persistent tile loop and spill)."""
     los, lens, taps, d, band, dense = info
-    nf, nc = d.shape[1], d.shape[0]
+    out = mel_bands(name, los, lens, dense, band, WAVES, "mel_band_code")
+    out += mel_bands(name, los, lens, dense, bands(lens, WAVES12), WAVES12, "mel_band12_code")
+    out += dct_groups(name, d, DCT_GROUPS, "dct_code")
+    return "\n".join(out)
+
+
+def mel_bands(name, los, lens, dense, band, waves, fname):
     out = []
     comp = "xyzw"
-    for w in range(WAVES):
+    for w in range(waves):
         fb, fe = band[w], band[w + 1]
-        out.append(f"template <> __device__ __forceinline__ void mel_band_code<{name}, {w}>(")
+        out.append(f"template <> __device__ __forceinline__ void {fname}<{name}, {w}>(")
         out.append("    const float* __restrict__ prow, float* __restrict__ lm) {")
         if fb == fe:
             out.append("  (void)prow;\n  (void)lm;\n}")
@@ -165,13 +179,13 @@ def emit_code(name, info):
                        f"  // (==0 -> eps), log10")
         out.append("}")
         out.append("")
-    out += dct_groups(name, d, DCT_GROUPS, "dct_code")
-    return "\n".join(out)
+    return out
 
 
 def dct_groups(name, d, ng, fname):
     """lifter x DCT of a log-mel row for the coefficient groups c = g + ng i
-    (ng = 4: waves 0..3 own four coefficients each)."""
+    (ng = 4: waves 0..3 own four coefficients each), one sequential fma chain
+    per coefficient (the MFMA DCT's order)."""
     nf, nc = d.shape[1], d.shape[0]
     per = (nc + ng - 1) // ng
     comp = "xyzw"
@@ -184,22 +198,20 @@ def dct_groups(name, d, ng, fname):
         for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
                        f"__builtin_assume_aligned(lm + {4 * q}, 16));")
-        chains = []  # (register, coefficient, filter parity)
+        # one fma chain per coefficient, filters in ascending order from +0:
+        # bit for bit the k-ordered chain of mfcc3_kernel's f32 MFMA DCT
+        # (v_mfma_f32_16x16x4_f32), so every clip path gives the same MFCCs
+        chains = []
         for i, c in enumerate(coefs):
-            out.append(f"  float a{i}, b{i};  // coefficient {c}: even / odd filters")
-            chains += [(f"a{i}", c, 0), (f"b{i}", c, 1)]
-        for step in range((nf + 1) // 2):
-            for reg, c, par in chains:
-                m = 2 * step + par
-                if m >= nf:
-                    continue
+            out.append(f"  float a{i} = 0.f;  // coefficient {c}")
+            chains.append((f"a{i}", c))
+        for m in range(nf):
+            for reg, c in chains:
                 q, r = divmod(m, 4)
                 src = f"q{q}.{comp[r]}"
-                op = "v_mul_f32_e32" if step == 0 else "v_fmac_f32_e32"
-                cons = "=v" if step == 0 else "+v"
-                out.append(f'  asm volatile("{op} %0, {bits(d[c, m])}, %1" : "{cons}"({reg}) : "v"({src}));')
+                out.append(f'  asm volatile("v_fmac_f32_e32 %0, {bits(d[c, m])}, %1" : "+v"({reg}) : "v"({src}));')
         for i in range(per):
-            out.append(f"  acc[{i}] = a{i} + b{i};" if i < len(coefs) else f"  acc[{i}] = 0.f;")
+            out.append(f"  acc[{i}] = a{i};" if i < len(coefs) else f"  acc[{i}] = 0.f;")
         out.append("}")
         out.append("")
     return out

@@ -82,17 +82,23 @@ class StreamBatch:
 
     def _hop_call(self, h, n_hops=1, labels=None):
         """vad_stream_hops with the per-batch arguments prepared once (the
-        Python side of a launch is a few microseconds of ctypes marshalling)."""
-        if getattr(self, "_hop_args", None) is None:
-            L, H = self.cfg.frame_size, self.cfg.hop
+        Python side of a launch is a few microseconds of ctypes marshalling:
+        per call only the hop block's address and strides change)."""
+        if getattr(self, "_hop_head", None) is None:
+            L = self.cfg.frame_size
             self._hop_fn = _lib.lib().vad_stream_hops
-            self._hop_args = (self.plan.handle, self.ffn.plan.handle, _lib.ptr(self.frames), L, L)
-        H = self.cfg.hop
+            self._hop_head = (self.plan.handle, self.ffn.plan.handle, _lib.ptr(self.frames), L, L)
+            self._hop_mid = (_lib.ptr(self.ring), _lib.ptr(self.count))
+            self._hop_labels = {}
         lab = self.labels if labels is None else labels
-        rc = self._hop_fn(*self._hop_args, ctypes.c_void_p(h.data_ptr()), h.stride(-2), H, self.n, n_hops,
-                          h.stride(0) if h.dim() == 3 else 0, _lib.ptr(self.ring), _lib.ptr(self.count),
-                          ctypes.c_void_p(lab.data_ptr()), lab.stride(0) if lab.dim() == 2 else 0,
-                          _lib.stream_ptr())
+        key = (lab.data_ptr(), n_hops)
+        tail = self._hop_labels.get(key)
+        if tail is None:
+            tail = (ctypes.c_void_p(lab.data_ptr()), lab.stride(0) if lab.dim() == 2 else 0)
+            self._hop_labels[key] = tail
+        rc = self._hop_fn(*self._hop_head, ctypes.c_void_p(h.data_ptr()), h.stride(-2), self.cfg.hop, self.n,
+                          n_hops, h.stride(0) if h.dim() == 3 else 0, *self._hop_mid, *tail,
+                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         if rc:
             _lib.check(rc, "vad_stream_hops")
 
