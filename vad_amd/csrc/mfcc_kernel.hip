@@ -57,6 +57,9 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 #ifndef VAD_NT_LOADS
 #define VAD_NT_LOADS 0
 #endif
+#ifndef VAD_DIAG_XP
+#define VAD_DIAG_XP 0  // diagnostic builds (VAD_DIAG_BUILD=10) only: see the paired-frame phase 1
+#endif
 template <typename TIN>
 struct Samples;
 template <>
@@ -290,7 +293,7 @@ __device__ __forceinline__ void load_chunks(const TIN* __restrict__ base, int li
   for (int c = B; c < E; ++c) {
     int o = 32 * c + 2 * n2;
     if (32 * c + 30 > LEN - 2) o = o < lim ? o : lim;
-    buf[c] = Samples<TIN>::raw_pair(base + o);
+    buf[c % NB] = Samples<TIN>::raw_pair(base + o);  // chunk c in slot c mod NB
   }
 }
 
@@ -544,6 +547,61 @@ __device__ __forceinline__ void phase2b(const MfccDev* __restrict__ plan, const 
   }
 }
 
+// lifter x DCT on the f32 matrix cores (v_mfma_f32_16x16x4_f32: exact f32,
+// a k-ordered fma chain, bit for bit the VALU dct_code chains), one 16-frame
+// block of log-mel rows per call: A = rows r0 .. r0 + 15 (lane l: row l & 15,
+// filter 4 s + l / 16), B = the [filter][16 coefficients] table dtb (zero past
+// the filters / coefficients; the rows' pad columns are zero), D[frame][coef]
+// (lane l: coefficient l & 15, frames 4 (l / 16) + r).  Row r0 + i is frame
+// f0 + r0 + i.
+template <int SPEC>
+constexpr int dct_k_steps() { return SPEC == 1 ? 7 : 10; }
+
+template <int SPEC>
+__device__ __forceinline__ void dct_mfma16(const float* __restrict__ lm, const float* __restrict__ dtb, int r0,
+                                           int lane, int64_t f0, int64_t f_end, float* __restrict__ out) {
+  constexpr int KS = dct_k_steps<SPEC>(), LMS = lm_stride<SPEC>(), MN = 13;
+  asm volatile("" : "+v"(lane));  // addresses per call (hoisted, they would stay live through the FFT)
+  const float* arow = lm + (r0 + (lane & 15)) * LMS + (lane >> 4);
+  const float* brow = dtb + (lane >> 4) * 16 + (lane & 15);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[4 * s], brow[64 * s], acc, 0, 0, 0);
+  const int c = lane & 15;
+  const int64_t fb = f0 + r0 + 4 * (lane >> 4);
+  if (c < MN) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (fb + r < f_end) out[(fb + r) * MN + c] = acc[r];
+  }
+}
+
+// the DCT table dtb and the zero pad columns of `rows` log-mel rows
+template <int SPEC>
+__device__ __forceinline__ void dct_mfma_setup(const MfccDev* __restrict__ plan, float* __restrict__ dtb,
+                                               float* __restrict__ lm, int rows, int tid, int nthreads) {
+  constexpr int KS = dct_k_steps<SPEC>(), LMS = lm_stride<SPEC>(), NF = SPEC == 1 ? 26 : 40, MN = 13;
+  static_assert(4 * KS >= NF && 4 * KS <= LMS, "DCT K steps");
+  for (int i = tid; i < 4 * KS * 16; i += nthreads) {
+    const int m = i >> 4, c = i & 15;
+    dtb[i] = (c < MN && m < NF) ? plan->dct[c * kMaxFilters + m] : 0.f;
+  }
+  for (int i = tid; i < rows * (LMS - NF); i += nthreads) lm[(i / (LMS - NF)) * LMS + NF + i % (LMS - NF)] = 0.f;
+}
+
+#ifndef VAD_DCT_MFMA
+#define VAD_DCT_MFMA 1  // 0: lifter x DCT on the VALU (dct_code) in mfcc_kernel too
+#endif
+// phase 2b of mfcc_kernel (waves 0..3 of a 64-frame tile): the MFMA form for
+// the compiled banks, else the VALU form
+template <int SPEC, bool STORE>
+__device__ __forceinline__ void phase2b_any(const MfccDev* __restrict__ plan, const float* lm, const float* dtb,
+                                            int wave, int lane, int64_t f0, int64_t n_frames, int mfcc_n,
+                                            float* __restrict__ out) {
+  if constexpr (SPEC >= 1 && STORE && VAD_DCT_MFMA) dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, f0, n_frames, out);
+  else phase2b<SPEC, STORE>(plan, lm, wave, lane, f0, n_frames, mfcc_n, out);
+}
+
 // In-kernel timestamps for DIAG 5/6 (diagnostic builds only): every wave
 // takes s_memtime at phase boundaries into SGPRs; lane 0 stores them at the
 // end of each of its first 8 tiles into `out` as [block][wave][tile][16]
@@ -618,6 +676,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
   float* P = reinterpret_cast<float*>(smem);                      // [64][260] power rows
   v2f* scr = reinterpret_cast<v2f*>(smem + kPBytes);              // FFT transposes
   float* lm = reinterpret_cast<float*>(smem + kPBytes + kScrBytes);  // [64][LMS] log-mel
+  float* dtb = lm + kTile * lm_stride<SPEC>();  // the MFMA DCT's operand table (SPEC 1 / 2), inside the log-mel region
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -629,6 +688,10 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
   const int len = frame_len < kFftN ? frame_len : kFftN;
   const int mfcc_n = plan->mfcc_n;
   const int64_t n_tiles = (n_frames + kTile - 1) / kTile;
+  if constexpr (MODE == kAudioToMfcc && SPEC >= 1 && VAD_DCT_MFMA) {
+    static_assert(kTile * lm_stride<SPEC>() + 4 * dct_k_steps<SPEC>() * 16 <= kLmFloats, "DCT table in the log-mel region");
+    dct_mfma_setup<SPEC>(plan, dtb, lm, kTile, tid, kThreads);  // read after the first tile's barriers
+  }
 
   if constexpr (MODE == kSpecToMfcc) {
     for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -727,41 +790,75 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       const TIN* nb = pair_base(tile + 1, lim);
       if (active) {  // phase 1
         v2f u[16], col[32];
+        // diagnostic builds (DIAG 10 only): XP 1 no LDS transposes (col from
+        // u in registers), XP 3 no FFT arithmetic (loads and LDS traffic only)
+        auto xpose = [&]() __attribute__((always_inline)) {
+          if constexpr (DIAG == 10 && (VAD_DIAG_XP == 1 || VAD_DIAG_XP == 4)) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) {
+              col[i] = u[i & 15];
+              asm volatile("" : "+v"(col[i]));
+            }
+          } else {
+            store_a(u, gscr, j);
+            read_b(L, gscr, col);
+          }
+        };
+        auto sa = [&](auto off) __attribute__((always_inline)) {
+          constexpr int OFF = decltype(off)::value;
+          if constexpr (DIAG == 10 && (VAD_DIAG_XP == 3 || VAD_DIAG_XP == 4)) {
+#pragma unroll
+            for (int n = 0; n < 16; ++n) {
+              u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);
+              asm volatile("" : "+v"(u[n]));
+            }
+          } else {
+            stage_a_at<TIN, NZ, LEN, OFF, NB, WIN>(buf, L, j, u, wv);
+          }
+        };
+        auto fb_ = [&](float* prow) __attribute__((always_inline)) {
+          if constexpr (DIAG == 10 && VAD_DIAG_XP == 4) {
+            if (col[3].x == 1234.5f) prow[L.e0] = col[7].y;  // keep the loads live, no LDS traffic
+          } else if constexpr (DIAG == 10 && VAD_DIAG_XP == 3) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) prow[L.e0 + 16 * i] = col[i].x + col[16 + i].y;
+          } else {
+            finish_b<MODE == kAudioToSpec>(L, col, prow);
+          }
+        };
         VAD_STAMP(0);
         VAD_MILESTONE(3);
-        stage_a_at<TIN, NZ, LEN, 0, NB, WIN>(buf, L, j, u, wv);
+        sa(std::integral_constant<int, 0>{});
         VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
-        load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
-        store_a(u, gscr, j);
-        read_b(L, gscr, col);
+        xpose();
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(2);
         VAD_MILESTONE(2);
         // pass 1's stage A covers the latency of pass 0's transpose reads
-        stage_a_at<TIN, NZ, LEN, HOPC, NB, WIN>(buf, L, j, u, wv);
+        sa(std::integral_constant<int, HOPC>{});
         __builtin_amdgcn_sched_barrier(0);
-        load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
+        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(3);
         VAD_MILESTONE(1);
-        if (MODE != kAudioToSpec || fa < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+        if (MODE != kAudioToSpec || fa < f_end) fb_(prow_a);
         __builtin_amdgcn_sched_barrier(0);
-        load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(4);
         VAD_MILESTONE(0);
-        store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
-        read_b(L, gscr, col);
+        xpose();  // after pass 0's reads in program order (LDS is in order per wave)
         VAD_STAMP(5);
-        if (MODE != kAudioToSpec || fb < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
+        if (MODE != kAudioToSpec || fb < f_end) fb_(prow_b);
       }
       if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(6);
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, f_end, mfcc_n, out);
+          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -783,7 +880,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
 
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, f_end, mfcc_n, out);
+        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
     }
     if constexpr (DIAG == 9) {
       __syncthreads();
@@ -929,7 +1026,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         // first (waves 0..3 are older and win VALU arbitration on their
         // SIMD) while their SIMD partners are still in their FFT
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -949,7 +1046,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     }
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -1203,9 +1300,6 @@ constexpr int kTile3 = 2 * kGroups3;       // 96 frames
 constexpr int kRegion3 = 2 * kGroupScratch;  // floats per group block (576 = 2304 B)
 constexpr int kLmRows3 = 128;              // frames 0..63, then 64..95 (+ 32 unused rows)
 
-// lifter x DCT as f32 MFMA B operand: [filter m][16 coefficients], K padded to 4
-template <int SPEC>
-constexpr int dct_k_steps() { return SPEC == 1 ? 7 : 10; }
 template <int SPEC>
 constexpr size_t mfcc3_smem_bytes() {
   return (size_t)kGroups3 * kRegion3 * sizeof(float) + (size_t)kLmRows3 * lm_stride<SPEC>() * sizeof(float) +
@@ -1231,7 +1325,7 @@ template <typename TIN, int NZ, int LEN, int OFF, int NB>
 __device__ __forceinline__ void stage_a_lds(const v2f (&buf)[NB], const v4f* __restrict__ twa4, int j,
                                             v2f (&u)[16]) {
 #pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[OFF + n]);
+  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);  // chunk c in slot c mod NB
   pad_stage_a<NZ, LEN, 16>(LEN, j, u);
   pk::dft16<NZ>(u);
 #pragma unroll
@@ -1240,6 +1334,60 @@ __device__ __forceinline__ void stage_a_lds(const v2f (&buf)[NB], const v4f* __r
     if (q > 0) u[2 * q] = pk::cmul(u[2 * q], t.xy);
     u[2 * q + 1] = pk::cmul(u[2 * q + 1], t.zw);
   }
+}
+
+// one 16-entry column of a transpose block (8 ds_read_b128)
+__device__ __forceinline__ void read_col(int c, const v2f* __restrict__ scr, v2f (&col)[16]) {
+  const v4f* cp = reinterpret_cast<const v4f*>(__builtin_assume_aligned(scr + c * kColStride, 16));
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const v4f t = cp[q];
+    col[2 * q] = t.xy;
+    col[2 * q + 1] = t.zw;
+  }
+}
+
+// the real-FFT split + power of finish_b on E (even half of column cE) and O
+// (odd half of column cO), twiddles W512^kE(m) from registers (TWB) or LDS
+template <bool TWREG>
+__device__ __forceinline__ void split_pw(const LaneConsts& L, const v4f* __restrict__ twb4, const v2f (&E)[8],
+                                         const v2f (&O)[8], float (&pkv)[8], float (&pnv)[8]) {
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    v2f tw;
+    if constexpr (TWREG) {
+      tw = L.twb[m];
+    } else {
+      const v4f tq = twb4[m >> 1];
+      tw = (m & 1) ? tq.zw : tq.xy;
+    }
+    const v2f a = (m >= 4 && L.col0) ? O[m] : E[m];
+    const v2f b = (m < 4 && L.col0) ? E[m == 0 ? 4 : (8 - m) & 7] : O[7 - m];
+    const v2f S = pk::add_conj(a, b);
+    const v2f T = pk::cmul(pk::sub_conj(a, b), tw);
+    const v2f U = pk::split_u(S, T);
+    const v2f V = pk::split_v(S, T);
+    const v2f p2 = U * U + V * V;
+    float pk = p2.x, pn = p2.y;
+    if (m == 0) {  // lane 14: bins 0 and 128 are their own partners
+      const float s0 = a.x + a.y;
+      pk = L.col0 ? 4.f * s0 * s0 : pk;
+      pn = L.col0 ? 4.f * fmaf(b.x, b.x, b.y * b.y) : pn;
+    }
+    pkv[m] = pk;
+    pnv[m] = pn;
+  }
+}
+
+// stage A with the per-lane twiddles in registers
+template <typename TIN, int NZ, int LEN, int OFF, int NB>
+__device__ __forceinline__ void stage_a_reg(const v2f (&buf)[NB], const LaneConsts& L, int j, v2f (&u)[16]) {
+#pragma unroll
+  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);  // chunk c in slot c mod NB
+  pad_stage_a<NZ, LEN, 16>(LEN, j, u);
+  pk::dft16<NZ>(u);
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
 }
 
 // finish_b's arithmetic with W512^kE(m) read from the LDS table; the 16
@@ -1292,6 +1440,18 @@ __device__ __forceinline__ void store_pw(const LaneConsts& L, const float (&pkv)
 #ifndef VAD_M3_PRIO
 #define VAD_M3_PRIO 1  // milestone priorities 3 -> 0 through phase 1 (lagging waves catch up)
 #endif
+#ifndef VAD_M3_TW
+#define VAD_M3_TW 0  // per-lane FFT twiddles: 0 both tables from LDS, 1 stage A's in VGPRs, 2 both in VGPRs
+#endif
+#ifndef VAD_M3_DIAG
+#define VAD_M3_DIAG 0  // diagnostic builds only (outputs wrong): 1 phase 1 alone, 2 phase 1 + barriers
+#endif
+#ifndef VAD_M3_BUF13
+#define VAD_M3_BUF13 0  // 1: 13 sample slots (pass 1's last 5 chunks loaded during the tile) instead of 18
+#endif
+#ifndef VAD_M3_SPLITREAD
+#define VAD_M3_SPLITREAD 0  // 1: column cE read and its even half computed before column cO is read
+#endif
 #define M3_PRIO(k)                                       \
   do {                                                   \
     if constexpr (VAD_M3_PRIO != 0) {                    \
@@ -1306,15 +1466,14 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
                                                              const TIN* __restrict__ src, int64_t n_frames,
                                                              float* __restrict__ out) {
   using T = std::conditional_t<SPEC == 1, Mel26, Mel40>;
-  constexpr int LEN = 400, NZ = 13, HOPC = 5, NB = NZ + HOPC, LMS = lm_stride<SPEC>();
+  constexpr int LEN = 400, NZ = 13, HOPC = 5, NC18 = NZ + HOPC, LMS = lm_stride<SPEC>();
+  constexpr int NB = VAD_M3_BUF13 ? NZ : NC18;  // sample slots (chunk c in slot c mod NB)
   constexpr int MN = T::NC;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* R = reinterpret_cast<float*>(smem);                 // 48 group blocks
   float* lm = R + kGroups3 * kRegion3;                        // [128][LMS] log-mel rows
   v2f* tw = reinterpret_cast<v2f*>(lm + kLmRows3 * LMS);      // per-lane twiddle table
   float* dtb = reinterpret_cast<float*>(tw) + 2 * 16 * (kTwaStride + kTwbStride);  // DCT operand table
-  constexpr int KS = dct_k_steps<SPEC>();
-  static_assert(4 * KS >= T::NF && 4 * KS <= LMS, "DCT K steps");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -1322,16 +1481,10 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
   const int grp = tid >> 4;
   const int j = tid & 15;
   stage_twiddles(plan, tw, tid, kThreads3);
-  // DCT table: B[m][c] = lifter x DCT[c][m] (zero past the filters / coefficients);
-  // the log-mel rows' pad columns are zeroed once (read against zero rows)
-  for (int i = tid; i < 4 * KS * 16; i += kThreads3) {
-    const int m = i >> 4, c = i & 15;
-    dtb[i] = (c < MN && m < T::NF) ? plan->dct[c * kMaxFilters + m] : 0.f;
-  }
-  for (int i = tid; i < kLmRows3 * (LMS - T::NF); i += kThreads3)
-    lm[(i / (LMS - T::NF)) * LMS + T::NF + i % (LMS - T::NF)] = 0.f;
+  dct_mfma_setup<SPEC>(plan, dtb, lm, kLmRows3, tid, kThreads3);  // the DCT operand table, zero pad columns
   LaneConsts L;
-  lane_ints(j, L);
+  if constexpr (VAD_M3_TW >= 1) lane_consts(plan, j, L);  // twiddles in VGPRs (all, or stage A's)
+  else lane_ints(j, L);
   const v4f* twa4 = reinterpret_cast<const v4f*>(tw + j * kTwaStride);
   const v4f* twb4 = reinterpret_cast<const v4f*>(tw + 16 * kTwaStride + j * kTwbStride);
 
@@ -1358,25 +1511,10 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
     return v;
   };
 
-  // lifter x DCT of a tile's log-mel rows on the f32 matrix cores
-  // (v_mfma_f32_16x16x4_f32: exact f32, a k-ordered fma chain), waves 0..5
-  // one 16-frame block each: A = log-mel rows 16 w .. 16 w + 15 (lane l:
-  // row l & 15, filter 4 s + l / 16), B = the table above, D[frame][coef]
-  // (lane l: coefficient l & 15, frames 4 (l / 16) + r)
+  // lifter x DCT of a tile's log-mel rows on the f32 matrix cores, waves
+  // 0..5 one 16-frame block each (log-mel rows 0..95 = the tile's frames)
   auto dct_store = [&](int64_t pf0) __attribute__((always_inline)) {
-    const int ln = opaque(lane);
-    const float* arow = lm + (16 * wave + (ln & 15)) * LMS + (ln >> 4);
-    const float* brow = dtb + (ln >> 4) * 16 + (ln & 15);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[4 * s], brow[64 * s], acc, 0, 0, 0);
-    const int c = lane & 15;
-    const int64_t fb = pf0 + 16 * wave + 4 * (lane >> 4);
-    if (c < MN) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (fb + r < f_end) out[(fb + r) * MN + c] = acc[r];
-    }
+    dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, f_end, out);
   };
 
   v2f buf[NB];
@@ -1386,46 +1524,84 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
     load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
   }
   __syncthreads();  // twiddle table staged
+  (void)NC18;
   int64_t prev_f0 = -1;
   for (int64_t tile = 0; tile < t_end; ++tile) {
     const int64_t f0 = f_beg + tile * kTile3;
     const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
-    int lim;
+    int lim, limc;
     const TIN* nb = pair_base(tile + 1, lim);
+    const TIN* cb = pair_base(tile, limc);
+    (void)cb;
     if (active) {
-      v2f u[16], col[32];
+      v2f u[16];
       float p0k[8], p0n[8];
+      auto stage_a = [&](auto off) __attribute__((always_inline)) {
+        constexpr int OFF = decltype(off)::value;
+        if constexpr (VAD_M3_TW >= 1) stage_a_reg<TIN, NZ, LEN, OFF, NB>(buf, L, j, u);
+        else stage_a_lds<TIN, NZ, LEN, OFF, NB>(buf, twa4, j, u);
+      };
+      // transpose reads + the even / odd half DFTs + split of one pass; `mid`
+      // runs once every read of the pass is issued (pass 1: pass 0's row store)
+      auto finish = [&](float (&pkv)[8], float (&pnv)[8], auto mid) __attribute__((always_inline)) {
+        v2f E[8], O[8];
+        if constexpr (VAD_M3_SPLITREAD) {
+          v2f col[16];
+          read_col(L.cE, gscr, col);
+          __builtin_amdgcn_sched_barrier(0);
+          pk::dft16_even(col, E);
+          __builtin_amdgcn_sched_barrier(0);
+          read_col(L.cO, gscr, col);
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          mid();
+          __builtin_amdgcn_sched_barrier(0);
+          pk::dft16_odd(col, O);
+        } else {
+          v2f col[32];
+          read_b(L, gscr, col);
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+          mid();
+          __builtin_amdgcn_sched_barrier(0);
+          pk::dft16_even(*reinterpret_cast<v2f(*)[16]>(&col[0]), E);
+          pk::dft16_odd(*reinterpret_cast<v2f(*)[16]>(&col[16]), O);
+        }
+        split_pw<VAD_M3_TW >= 2>(L, twb4, E, O, pkv, pnv);
+      };
       M3_PRIO(3);
-      stage_a_lds<TIN, NZ, LEN, 0, NB>(buf, twa4, j, u);
+      stage_a(std::integral_constant<int, 0>{});
       __builtin_amdgcn_sched_barrier(0);
-      load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+      if constexpr (VAD_M3_BUF13) load_chunks<TIN, NZ, NC18, LEN>(cb, limc, j, buf);  // this tile's 13..17
+      else load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
       store_a(u, gscr, j);
-      read_b(L, gscr, col);
       __builtin_amdgcn_sched_barrier(0);
       M3_PRIO(2);
-      finish_b_pw(L, twb4, col, p0k, p0n);
+      finish(p0k, p0n, [] {});
       __builtin_amdgcn_sched_barrier(0);
       M3_PRIO(1);
-      stage_a_lds<TIN, NZ, LEN, HOPC, NB>(buf, twa4, j, u);
+      stage_a(std::integral_constant<int, HOPC>{});
       __builtin_amdgcn_sched_barrier(0);
-      load_chunks<TIN, HOPC, NB, LEN>(nb, lim, j, buf);
+      if constexpr (VAD_M3_BUF13) load_chunks<TIN, 0, NZ, LEN>(nb, lim, j, buf);  // next tile's 0..12
+      else load_chunks<TIN, HOPC, NC18, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
       store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
-      read_b(L, gscr, col);
-      // pass 0's row: into the block after pass 1's transpose reads were issued
-      asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       M3_PRIO(0);
-      store_pw(L, p0k, p0n, prow0);
-      __builtin_amdgcn_sched_barrier(0);
       float p1k[8], p1n[8];
-      finish_b_pw(L, twb4, col, p1k, p1n);
+      // pass 0's row goes into the block once pass 1's transpose reads are issued
+      finish(p1k, p1n, [&] { store_pw(L, p0k, p0n, prow0); });
       store_pw(L, p1k, p1n, prow1);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
+    if constexpr (VAD_M3_DIAG == 1) continue;  // diagnostic builds: phase 1 only
+    if (VAD_M3_DIAG != 2 && prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
     lds_barrier();  // power rows complete; log-mel rows consumed
+    if constexpr (VAD_M3_DIAG == 2) {  // diagnostic builds: phase 1 and the barriers only
+      lds_barrier();
+      continue;
+    }
     // phase 2a: mel + log10, frame per lane
     {
       const int ln = opaque(lane);
@@ -1456,7 +1632,7 @@ static hipError_t launch_mfcc3(const MfccDev* plan, const TIN* src, int64_t n, f
 }
 
 #ifndef VAD_MFCC3
-#define VAD_MFCC3 1  // 0: the two-wave kernel for the reference framing (A/B builds)
+#define VAD_MFCC3 0  // 1: the 12-wave mfcc3_kernel for the reference framing (A/B builds)
 #endif
 
 size_t mfcc_smem_bytes() { return kPBytes + kScrBytes + kLmBytes; }  // 157,696 B
