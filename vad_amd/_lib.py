@@ -121,7 +121,14 @@ def ptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(stream=None):
-    """hipStream_t of a torch stream (default: the current stream)."""
+    """hipStream_t of a torch stream (default: the current stream of the
+    current device, read without building a Stream object: this sits on
+    every per-hop launch path)."""
+    if stream is None and _raw_stream is not None:
+        return ctypes.c_void_p(_raw_stream(torch.cuda.current_device()))
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)

@@ -57,6 +57,10 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 #ifndef VAD_NT_LOADS
 #define VAD_NT_LOADS 0
 #endif
+#ifndef VAD_DCT_AT
+#define VAD_DCT_AT 0  // where the paired-frame loop runs the deferred DCT (A/B builds): 0 waves 0..3
+                      // after phase 1, 1 waves 0..3 before it, 2 waves 4..7 after it
+#endif
 #ifndef VAD_DIAG_XP
 #define VAD_DIAG_XP 0  // diagnostic builds (VAD_DIAG_BUILD=10) only: see the paired-frame phase 1
 #endif
@@ -788,6 +792,14 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       }
       int lim;
       const TIN* nb = pair_base(tile + 1, lim);
+      // VAD_DCT_AT 1: the deferred DCT at the top of the tile (before phase 1)
+      // on its waves, 2: on waves 4..7 after phase 1 (A/B variants)
+      const int dct_wave = VAD_DCT_AT == 2 ? wave - 4 : wave;
+      if constexpr (MODE == kAudioToMfcc && DIAG != 10 && VAD_DCT_AT == 1) {
+        if (prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
+          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
+        __builtin_amdgcn_sched_barrier(0);
+      }
       if (active) {  // phase 1
         v2f u[16], col[32];
         // diagnostic builds (DIAG 10 only): XP 1 no LDS transposes (col from
@@ -857,8 +869,8 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
         __builtin_amdgcn_sched_barrier(0);
         VAD_STAMP(6);
-        if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
+        if (VAD_DCT_AT != 1 && prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
+          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
         VAD_STAMP(7);
         lds_barrier();  // P complete; log-mel rows consumed
         VAD_STAMP(8);
@@ -879,8 +891,9 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     for (; tile < t_end; ++tile, ++it) tile_body(buf);
 
     if constexpr (MODE == kAudioToMfcc) {
-      if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
+      const int dct_wave = VAD_DCT_AT == 2 ? wave - 4 : wave;
+      if (prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
+        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
     }
     if constexpr (DIAG == 9) {
       __syncthreads();
@@ -1452,6 +1465,14 @@ __device__ __forceinline__ void store_pw(const LaneConsts& L, const float (&pkv)
 #ifndef VAD_M3_SPLITREAD
 #define VAD_M3_SPLITREAD 0  // 1: column cE read and its even half computed before column cO is read
 #endif
+#define M3_STAMP(k)                                      \
+  do {                                                   \
+    if constexpr (VAD_M3_DIAG == 5) {                    \
+      __builtin_amdgcn_sched_barrier(0);                 \
+      st_[k] = __builtin_amdgcn_s_memtime();             \
+      __builtin_amdgcn_sched_barrier(0);                 \
+    }                                                    \
+  } while (0)
 #define M3_PRIO(k)                                       \
   do {                                                   \
     if constexpr (VAD_M3_PRIO != 0) {                    \
@@ -1514,7 +1535,8 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
   // lifter x DCT of a tile's log-mel rows on the f32 matrix cores, waves
   // 0..5 one 16-frame block each (log-mel rows 0..95 = the tile's frames)
   auto dct_store = [&](int64_t pf0) __attribute__((always_inline)) {
-    dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, f_end, out);
+    if constexpr (VAD_M3_DIAG == 5) dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, 0, out);  // stamps in `out`
+    else dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, f_end, out);
   };
 
   v2f buf[NB];
@@ -1527,6 +1549,9 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
   (void)NC18;
   int64_t prev_f0 = -1;
   for (int64_t tile = 0; tile < t_end; ++tile) {
+    unsigned long long st_[12];
+    (void)st_;
+    M3_STAMP(0);
     const int64_t f0 = f_beg + tile * kTile3;
     const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
     int lim, limc;
@@ -1575,17 +1600,20 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
       if constexpr (VAD_M3_BUF13) load_chunks<TIN, NZ, NC18, LEN>(cb, limc, j, buf);  // this tile's 13..17
       else load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
+      M3_STAMP(1);
       store_a(u, gscr, j);
       __builtin_amdgcn_sched_barrier(0);
       M3_PRIO(2);
       finish(p0k, p0n, [] {});
       __builtin_amdgcn_sched_barrier(0);
+      M3_STAMP(2);
       M3_PRIO(1);
       stage_a(std::integral_constant<int, HOPC>{});
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (VAD_M3_BUF13) load_chunks<TIN, 0, NZ, LEN>(nb, lim, j, buf);  // next tile's 0..12
       else load_chunks<TIN, HOPC, NC18, LEN>(nb, lim, j, buf);
       __builtin_amdgcn_sched_barrier(0);
+      M3_STAMP(3);
       store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
       __builtin_amdgcn_sched_barrier(0);
       M3_PRIO(0);
@@ -1595,9 +1623,12 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
       store_pw(L, p1k, p1n, prow1);
     }
     __builtin_amdgcn_sched_barrier(0);
+    M3_STAMP(4);
     if constexpr (VAD_M3_DIAG == 1) continue;  // diagnostic builds: phase 1 only
     if (VAD_M3_DIAG != 2 && prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
+    M3_STAMP(5);
     lds_barrier();  // power rows complete; log-mel rows consumed
+    M3_STAMP(6);
     if constexpr (VAD_M3_DIAG == 2) {  // diagnostic builds: phase 1 and the barriers only
       lds_barrier();
       continue;
@@ -1608,8 +1639,17 @@ __global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __re
       mel12_dispatch<T>(wave, R + row_off3(ln >> 1, ln & 1), lm + ln * LMS);
       mel12_dispatch<T>(wave, R + row_off3(32 + ((ln & 31) >> 1), ln & 1), lm + (64 + ln) * LMS);
     }
+    M3_STAMP(7);
     lds_barrier();  // log-mel rows complete; the blocks free
+    M3_STAMP(8);
     prev_f0 = f0;
+    if constexpr (VAD_M3_DIAG == 5) {  // stamps of tiles 0..7: [block][wave][tile][16] in `out`
+      unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
+      if (lane == 0 && tile < 8) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) stamps[(((size_t)blockIdx.x * kW3 + wave) * 8 + tile) * 16 + k] = st_[k];
+      }
+    }
   }
   if (prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
 }

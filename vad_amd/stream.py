@@ -98,7 +98,7 @@ class StreamBatch:
             self._hop_labels[key] = tail
         rc = self._hop_fn(*self._hop_head, ctypes.c_void_p(h.data_ptr()), h.stride(-2), self.cfg.hop, self.n,
                           n_hops, h.stride(0) if h.dim() == 3 else 0, *self._hop_mid, *tail,
-                          ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+                          _lib.stream_ptr())
         if rc:
             _lib.check(rc, "vad_stream_hops")
 
