@@ -178,6 +178,10 @@ __device__ __forceinline__ float2 w256(const float2* __restrict__ tw, int m) {
   return m < 128 ? t : make_float2(-t.x, -t.y);
 }
 
+// NR: 64-sample chunks of the frame a lane holds (7: frames up to 448
+// samples, the reference's 400; 16: up to 1024) -- the frame and the next
+// hop's samples stay in registers across hops, so the bound matters
+template <int NR>
 __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restrict__ blob, int blob_n, int nf,
                                                           int n_taps, FfnDev net,
                                                           float* __restrict__ frames, int64_t fstride, int len,
@@ -232,9 +236,9 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   // in the advanced frame, the frame count and the MFCC ring
   float* row = frames + sc * fstride;
   const int keep = len - hlen;
-  float v[16], hn[16];
+  float v[NR], hn[NR];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int t = lane + 64 * i;
     v[i] = t < len ? row[t] : 0.f;
     hn[i] = (t >= keep && t < len) ? hop[sc * hstride + (t - keep)] : 0.f;
@@ -258,39 +262,44 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   // K hops of this stream back to back: the same computation per hop as K
   // launches of one hop (state carried in registers), the tables staged once
   for (int k = 0; k < n_hops; ++k) {
+    // the lane index, opaque per hop: otherwise the compiler hoists every
+    // lane-dependent LDS address of the hop out of the loop and runs out of
+    // registers holding them
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
     // -- frame: shift by the hop (through LDS: sample t + hlen belongs to
-    // another lane), append the new samples (stream_push_kernel)
+    // another ln), append the new samples (stream_push_kernel)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int t = lane + 64 * i;
+    for (int i = 0; i < NR; ++i) {
+      const int t = ln + 64 * i;
       if (t < len) fb[t] = v[i];
     }
     asm volatile("" ::: "memory");
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int t = lane + 64 * i;
+    for (int i = 0; i < NR; ++i) {
+      const int t = ln + 64 * i;
       v[i] = t < keep ? fb[t + hlen] : hn[i];
     }
     asm volatile("" ::: "memory");
     if (k + 1 < n_hops) {  // the next hop's samples, in flight during this one
       const float* hs = hop + (int64_t)(k + 1) * hop_kstride + s * hstride;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int t = lane + 64 * i;
+      for (int i = 0; i < NR; ++i) {
+        const int t = ln + 64 * i;
         hn[i] = (t >= keep && t < len) ? hs[t - keep] : 0.f;
       }
     }
     uint8_t* lab_k = labels + (int64_t)k * lab_kstride;
     if (VAD_HOP_DIAG == 1) {
-      if (lane == 0) lab_k[s] = (uint8_t)v[0];
+      if (ln == 0) lab_k[s] = (uint8_t)v[0];
       continue;
     }
     // samples of the FFT (np.fft.fft(x, 512): zero-pad / truncate, mfcc.py:61)
     float* xs = reinterpret_cast<float*>(z1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int t = lane + 64 * i;  // sample t = component t & 1 of complex t / 2
-      xs[2 * zp(t >> 1) + (t & 1)] = t < used ? v[i] : 0.f;
+    for (int i = 0; i < 8; ++i) {  // all 512 inputs: the zero padding past the frame too
+      const int t = ln + 64 * i;  // sample t = component t & 1 of complex t / 2
+      xs[2 * zp(t >> 1) + (t & 1)] = (i < NR && t < used) ? v[i < NR ? i : 0] : 0.f;
     }
     // LDS is in order within a wave; these keep the compiler from moving
     // accesses of one phase (other lanes' data, other element types) across
@@ -303,8 +312,8 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const int ns = 1 << (2 * st);  // 1, 4, 16, 64
-      const int kk = lane & (ns - 1);
-      float2 a0 = src[zp(lane)], a1 = src[zp(lane + 64)], a2 = src[zp(lane + 128)], a3 = src[zp(lane + 192)];
+      const int kk = ln & (ns - 1);
+      float2 a0 = src[zp(ln)], a1 = src[zp(ln + 64)], a2 = src[zp(ln + 128)], a3 = src[zp(ln + 192)];
       if (st > 0) {
         const int m = kk * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
         a1 = cmulf(a1, w256(T.tw, m));
@@ -313,7 +322,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       }
       const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
       const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
-      const int o = (lane >> (2 * st)) * (4 * ns) + kk;
+      const int o = (ln >> (2 * st)) * (4 * ns) + kk;
       dst[zp(o)] = make_float2(b0.x + b2.x, b0.y + b2.y);
       dst[zp(o + ns)] = make_float2(b1.x + b3.y, b1.y - b3.x);      // b1 - i b3
       dst[zp(o + 2 * ns)] = make_float2(b0.x - b2.x, b0.y - b2.y);
@@ -324,7 +333,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       asm volatile("" ::: "memory");
     }
     if (VAD_HOP_DIAG == 2) {
-      if (lane == 0) lab_k[s] = (uint8_t)src[3].x;
+      if (ln == 0) lab_k[s] = (uint8_t)src[3].x;
       continue;
     }
     // -- real-FFT split: 2X[k] = S - i W512^k D, S = Z[k] + conj(Z[-k]),
@@ -333,7 +342,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     float pk[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int kb = lane + 64 * q;
+      const int kb = ln + 64 * q;
       const float2 zk = src[zp(kb)], zn = src[zp((256 - kb) & 255)];
       const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
       const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
@@ -342,36 +351,36 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       pk[q] = fmaf(u, u, vv * vv);
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pw[lane + 64 * q] = pk[q];
+    for (int q = 0; q < 4; ++q) pw[ln + 64 * q] = pk[q];
     asm volatile("" ::: "memory");
-    // -- mel + log10 (lane m), lifter x DCT (lane c)
-    if (lane < nf) {
-      const int lo = T.f_lo[lane], n = T.f_len[lane];
-      const float* wt = T.taps + T.f_off[lane];
+    // -- mel + log10 (ln m), lifter x DCT (ln c)
+    if (ln < nf) {
+      const int lo = T.f_lo[ln], n = T.f_len[ln];
+      const float* wt = T.taps + T.f_off[ln];
       // unrolled: the LDS reads of a batch are in flight together (a rolled
       // loop waits one LDS round trip per tap)
       float e = 0.f;
 #pragma unroll 8
       for (int t = 0; t < n; ++t) e = fmaf(wt[t], pw[lo + t], e);
-      lmr[lane] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
+      lmr[ln] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
     }
     asm volatile("" ::: "memory");
     float mf = 0.f;
-    if (lane < mfcc_n) {
-      const float* d = T.dct + lane * nf;
+    if (ln < mfcc_n) {
+      const float* d = T.dct + ln * nf;
 #pragma unroll 8
       for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
     }
 
     if (VAD_HOP_DIAG == 3) {
-      if (lane == 0) lab_k[s] = (uint8_t)mf;
+      if (ln == 0) lab_k[s] = (uint8_t)mf;
       continue;
     }
     // -- window of the five previous frames, then push the new row
     const bool have = c >= 5;
-    act_a[lane] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
+    act_a[ln] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
     asm volatile("" ::: "memory");
-    if (lane < mfcc_n) {
+    if (ln < mfcc_n) {
       if (have) {
         // slot (c + d) % 5, d = 0..4: the ring in arrival order, oldest first
         float r[5];
@@ -381,9 +390,9 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
           r[d] = q == 0 ? rv[0] : q == 1 ? rv[1] : q == 2 ? rv[2] : q == 3 ? rv[3] : rv[4];
         }
         const Feat3 ft = feature_triple(r[0], r[1], r[2], r[3], r[4], VAD_FEAT_ANALYSER);
-        act_a[lane] = ft.mn;
-        act_a[mfcc_n + lane] = ft.d1;
-        act_a[2 * mfcc_n + lane] = ft.d2;
+        act_a[ln] = ft.mn;
+        act_a[mfcc_n + ln] = ft.d1;
+        act_a[2 * mfcc_n + ln] = ft.d2;
       }
       const int q = c % 5;  // the push (ring slot of the oldest row)
 #pragma unroll
@@ -396,12 +405,12 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       // not the delta columns, in the rest of its last block (stored after the
       // features: LDS is in order per wave)
       const int din0 = net.dims[0];
-      if (lane >= din0 && lane < ((din0 + 3) & ~3)) act_a[lane] = 0.f;
+      if (ln >= din0 && ln < ((din0 + 3) & ~3)) act_a[ln] = 0.f;
     }
     asm volatile("" ::: "memory");
     uint8_t label = 255;
     if (have && VAD_HOP_DIAG != 4) {
-      // -- FFN: exact f32, lane o of each layer
+      // -- FFN: exact f32, ln o of each layer
       float* hin = act_a;
       float* hout = act_b;
       const int nl = net.n_layers;
@@ -412,19 +421,19 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
         // the next finite values of the block (zero-padded at its end)
         const float* W = T.w + net.woff[l];
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-        if (lane < dout) {
+        if (ln < dout) {
           const float4* h4 = reinterpret_cast<const float4*>(hin);
 #pragma unroll 4
           for (int kq = 0; kq < din; kq += 4) {
             const float4 h = h4[kq >> 2];
-            a0 = fmaf(W[kq * dout + lane], h.x, a0);
-            a1 = fmaf(W[(kq + 1) * dout + lane], h.y, a1);
-            a2 = fmaf(W[(kq + 2) * dout + lane], h.z, a2);
-            a3 = fmaf(W[(kq + 3) * dout + lane], h.w, a3);
+            a0 = fmaf(W[kq * dout + ln], h.x, a0);
+            a1 = fmaf(W[(kq + 1) * dout + ln], h.y, a1);
+            a2 = fmaf(W[(kq + 2) * dout + ln], h.z, a2);
+            a3 = fmaf(W[(kq + 3) * dout + ln], h.w, a3);
           }
         }
-        const float acc = T.w[net.boff[l] + (lane < dout ? lane : 0)] + ((a0 + a1) + (a2 + a3));
-        hout[lane] = lane < dout ? (l + 1 < nl ? relu_nan(acc) : acc) : 0.f;
+        const float acc = T.w[net.boff[l] + (ln < dout ? ln : 0)] + ((a0 + a1) + (a2 + a3));
+        hout[ln] = ln < dout ? (l + 1 < nl ? relu_nan(acc) : acc) : 0.f;
         float* t = hin;
         hin = hout;
         hout = t;
@@ -434,13 +443,13 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
                         hin[3 < net.n_classes ? 3 : 0]};
       label = (uint8_t)argmax_classes(zl, net.n_classes);
     }
-    if (lane == 0) lab_k[s] = label;
+    if (ln == 0) lab_k[s] = label;
     c = (c + 1 >= 10) ? c + 1 - 5 : c + 1;
     asm volatile("" ::: "memory");
   }
   // -- the stream's state back: frame, ring, count
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
+  for (int i = 0; i < NR; ++i) {
     const int t = lane + 64 * i;
     if (t < len) row[t] = v[i];
   }
@@ -486,12 +495,21 @@ hipError_t launch_stream_hop(const MfccDev* plan, const float* blob, int blob_n,
   const size_t smem = tables + (size_t)waves * kHopWaveFloats * sizeof(float);
   if (smem > 160 * 1024) return hipErrorInvalidValue;
   static std::atomic<unsigned long long> attr_done{0};
-  const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&stream_hop_kernel), 160 * 1024, attr_done);
+  static std::atomic<unsigned long long> attr_done16{0};
+  const bool small = len <= 7 * 64;
+  const void* fn = small ? reinterpret_cast<const void*>(&stream_hop_kernel<7>)
+                         : reinterpret_cast<const void*>(&stream_hop_kernel<16>);
+  const hipError_t e = ensure_dyn_lds(fn, 160 * 1024, small ? attr_done : attr_done16);
   if (e != hipSuccess) return e;
   const dim3 grid((unsigned)((n_streams + waves - 1) / waves));
-  hipLaunchKernelGGL(stream_hop_kernel, grid, dim3(64 * waves), smem, st, blob, blob_n, nf, n_taps, net, frames,
-                     fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels, n_hops, hop_kstride,
-                     lab_kstride);
+  if (small)
+    hipLaunchKernelGGL(stream_hop_kernel<7>, grid, dim3(64 * waves), smem, st, blob, blob_n, nf, n_taps, net, frames,
+                       fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels, n_hops, hop_kstride,
+                       lab_kstride);
+  else
+    hipLaunchKernelGGL(stream_hop_kernel<16>, grid, dim3(64 * waves), smem, st, blob, blob_n, nf, n_taps, net, frames,
+                       fstride, len, hop, hstride, hlen, n_streams, mfcc_n, ring, count, labels, n_hops, hop_kstride,
+                       lab_kstride);
   return hipGetLastError();
 }
 
