@@ -59,10 +59,16 @@ def build(force=False, verbose=True, defines=(), out=None):
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     base = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
             "-Wno-unused-function"]
+    # experiment variants: VAD_UNIT_FLAGS="unit.hip:-flag,-flag;unit2.hip:..." adds per-unit flags
+    extra = {}
+    for item in filter(None, os.environ.get("VAD_UNIT_FLAGS", "").split(";")):
+        unit, _, flags = item.partition(":")
+        extra[unit] = flags.split(",")
     procs, objs = [], []
     for name in SOURCES:  # one object per unit, compiled in parallel
         obj = os.path.join(LIB_DIR, os.path.basename(lib) + "." + name.replace(".hip", ".o"))
-        cmd = base + list(defines) + UNIT_FLAGS.get(name, []) + ["-c", os.path.join(CSRC, name), "-o", obj]
+        cmd = base + list(defines) + UNIT_FLAGS.get(name, []) + extra.get(name, []) + \
+            ["-c", os.path.join(CSRC, name), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append(subprocess.Popen(cmd))
