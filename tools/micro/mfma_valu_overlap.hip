@@ -72,6 +72,8 @@ __global__ void k(float* out, int mode, int iters_v, int iters_m) {
   else if (mode == 7) { if (!older) svalu_work(out, iters_v); }
   else if (mode == 8) { if (older) mfma16_work(out, iters_m); else svalu_work(out, iters_v); }
   else if (mode == 9) { if (older) svalu_work(out, iters_v); else svalu_work(out, iters_v); }
+  else if (mode == 10) { if (older) mfma16_work(out, iters_m); else valu_work(out, iters_v); }
+  else if (mode == 11) { if (older) mfma_work(out, iters_m); else svalu_work(out, iters_v); }
 }
 
 int main() {
@@ -84,9 +86,10 @@ int main() {
   const int im = 20000;  // 8k MFMA per wave (x32 cyc = 256k cyc)
   const char* names[] = {"both VALU", "both MFMA", "old MFMA + young VALU", "old MFMA only",
                          "young VALU only", "old VALU + young MFMA", "old f16 MFMA only",
-                         "young scalar VALU only", "old f16 MFMA + young scalar", "both scalar VALU"};
-  for (int mm = 0; mm < 20; ++mm) {
-    const int mode = mm % 10;
+                         "young scalar VALU only", "old f16 MFMA + young scalar", "both scalar VALU",
+                         "old f16 MFMA + young pk", "old f32 MFMA + young scalar"};
+  for (int mm = 0; mm < 24; ++mm) {
+    const int mode = mm % 12;
     float best = 1e30f;
     for (int rep = 0; rep < 4; ++rep) {
       (void)hipEventRecord(e0);
