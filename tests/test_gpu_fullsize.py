@@ -75,6 +75,28 @@ def test_c2_mfcc_every_frame(torch_cuda, nf):
     assert_mfcc_close(plan.clip_mfcc(a32).cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("word", ["0x80ff80ff80ff80ff", "0xffffffffffffff80", "0x8090a0b0c0d0e0ff"])
+@pytest.mark.parametrize("F", [100_000, 12_345, 300])
+def test_xcd_balanced_runs_cover_every_frame(torch_cuda, monkeypatch, word, F):
+    """The MFCC kernel's XCD-balanced tile runs (vad_common.h MfccBalance)
+    partition the tiles exactly whatever the weights: forced extreme weights
+    give bit-identical MFCCs to equal runs, for grids of 256 workgroups and
+    of fewer (12,345 frames: 193; 300: 5), and the adaptive default too."""
+    torch = torch_cuda
+    from vad_amd.plan import MfccPlan
+    clip = O.synth_clip(O.samples_for_frames(F), seed=5)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    a32 = torch.from_numpy(clip).cuda()
+    monkeypatch.setenv("VAD_MFCC_BALANCE", "0")
+    want = MfccPlan(fb).clip_mfcc(a32)
+    monkeypatch.setenv("VAD_MFCC_BALANCE", "1")
+    adaptive = MfccPlan(fb)
+    for _ in range(4):  # weights adapt from the stats of the launches before
+        assert torch.equal(adaptive.clip_mfcc(a32), want)
+    monkeypatch.setenv("VAD_MFCC_BALANCE_WORD", word)
+    assert torch.equal(MfccPlan(fb).clip_mfcc(a32), want)
+
+
 def test_c3_full_clip_vs_oracle(torch_cuda):
     """C3 (BASELINE configs[2]): 1M frames, 13-64-64-2 with the bench's
     weights; MFCCs of every frame and labels of every window vs the oracle

@@ -29,6 +29,7 @@ e.record()
 torch.cuda.synchronize()
 wall_us = s.elapsed_time(e) * 1e3
 st = buf[F * 13:].view(torch.int64).cpu().numpy().reshape(1024, 4).astype(np.float64)
+blk = np.nonzero(st[:, 1] > 0)[0]
 st = st[st[:, 1] > 0]  # launched workgroups
 t0, r0, t1, r1 = st[:, 0], st[:, 1], st[:, 2], st[:, 3]
 clk = (t1 - t0) / ((r1 - r0) / 100e6) / 1e9  # s_memrealtime: 100 MHz
@@ -39,3 +40,9 @@ print(f"wall {wall_us:.1f} us; shader clock median {np.median(clk):.3f} GHz (min
 print(f"workgroup duration us: min {dur_us.min():.1f} median {np.median(dur_us):.1f} max {dur_us.max():.1f}")
 print(f"start skew us: max {start_us.max():.1f}; end spread: first {end_us.min():.1f} last {end_us.max():.1f}")
 print("workgroups", len(st), "cycles per workgroup: median", np.median(t1 - t0))
+cyc = t1 - t0
+print(f"cycles per workgroup: min {cyc.min():.0f} max {cyc.max():.0f}")
+for x in range(8):  # workgroups are dealt to the 8 XCDs round-robin (block b -> XCD b mod 8)
+    m = blk % 8 == x
+    print(f"XCD {x}: clock {np.median(clk[m]):.3f} GHz, duration median {np.median(dur_us[m]):.1f} "
+          f"max {dur_us[m].max():.1f} us, cycles median {np.median(cyc[m]):.0f}")

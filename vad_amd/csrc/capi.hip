@@ -3,15 +3,126 @@
 // (filterbank -> sparse taps, lifter x DCT matrix, twiddles, FFN fragments);
 // every hot entry point only validates and launches.
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <vector>
 
 #include "vad_common.h"
 #include "mel_tables.h"
 
 using namespace vad;
+
+// Host side of the MFCC kernel's XCD balance (vad_common.h MfccBalance):
+// the kernel's paired-frame runs write (tiles, ticks) per workgroup into
+// host-mapped memory; each launch folds the latest ones into per-XCD speed
+// weights (workgroup b on XCD b mod 8) and passes them as a kernel argument,
+// so every workgroup of a launch splits the tiles from the same 8 bytes.
+// VAD_MFCC_BALANCE=0 turns it off (equal runs, no stats).
+#ifndef VAD_BALANCE_DEFAULT
+#define VAD_BALANCE_DEFAULT 1
+#endif
+namespace {
+constexpr int kBalSlots = 1024;  // workgroups of a launch (<= CUs)
+struct BalanceHost {
+  unsigned long long* stats_host = nullptr;  // pinned, mapped
+  unsigned long long* stats_dev = nullptr;
+  float w[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  unsigned long long forced = 0;  // VAD_MFCC_BALANCE_WORD (tests): fixed weights
+  std::mutex mu;
+};
+
+BalanceHost* balance_create() {
+  const char* env = getenv("VAD_MFCC_BALANCE");
+  if (env ? atoi(env) == 0 : VAD_BALANCE_DEFAULT == 0) return nullptr;
+  BalanceHost* b = new BalanceHost();
+  void* h = nullptr;
+  if (hipHostMalloc(&h, kBalSlots * sizeof(unsigned long long), hipHostMallocMapped) != hipSuccess) {
+    delete b;
+    return nullptr;
+  }
+  memset(h, 0, kBalSlots * sizeof(unsigned long long));
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+    (void)hipHostFree(h);
+    delete b;
+    return nullptr;
+  }
+  b->stats_host = (unsigned long long*)h;
+  b->stats_dev = (unsigned long long*)d;
+  if (const char* fw = getenv("VAD_MFCC_BALANCE_WORD")) {
+    b->forced = strtoull(fw, nullptr, 0);
+    for (int x = 0; x < 8; ++x)  // every weight >= 1, or no forcing
+      if (((b->forced >> (8 * x)) & 255u) == 0) b->forced = 0;
+  }
+  return b;
+}
+
+void balance_destroy(BalanceHost* b) {
+  if (!b) return;
+  (void)hipHostFree(b->stats_host);
+  delete b;
+}
+
+// this launch's weights from the stats the earlier launches left (a launch
+// still running leaves some of its blocks' entries old: any mix is a valid,
+// if less even, split)
+MfccBalance balance_for_launch(BalanceHost* b) {
+  MfccBalance r;
+  if (!b) return r;
+  if (b->forced) {
+    r.word = b->forced;
+    r.stats = b->stats_dev;
+    return r;
+  }
+  std::lock_guard<std::mutex> lk(b->mu);
+  double tiles[8] = {}, ticks[8] = {};
+  const volatile unsigned long long* st = b->stats_host;
+  for (int i = 0; i < kBalSlots; ++i) {
+    const unsigned long long v = st[i];
+    if (!v) continue;
+    tiles[i & 7] += (double)(v >> 40);
+    ticks[i & 7] += (double)(v & ((1ull << 40) - 1));
+  }
+  bool all = true;
+  double sp[8], mx = 0.;
+  for (int x = 0; x < 8; ++x) {
+    all = all && tiles[x] > 0. && ticks[x] > 0.;
+    sp[x] = ticks[x] > 0. ? tiles[x] / ticks[x] : 0.;
+    mx = sp[x] > mx ? sp[x] : mx;
+  }
+  if (all && mx > 0.) {
+    for (int x = 0; x < 8; ++x) {
+      // each launch ran on the previous weights: a block's speed is its
+      // tiles per tick whatever its share, so the new weights are the speeds
+      // (smoothed: the clocks drift with load and temperature)
+      b->w[x] = 0.5f * b->w[x] + 0.5f * (float)(sp[x] / mx);
+    }
+  }
+  float wm = 0.f;
+  for (int x = 0; x < 8; ++x) wm = b->w[x] > wm ? b->w[x] : wm;
+  unsigned long long word = 0;
+  for (int x = 0; x < 8; ++x) {
+    int q = (int)lrintf(255.f * b->w[x] / wm);
+    q = q < 128 ? 128 : (q > 255 ? 255 : q);  // at most a 2x spread
+    word |= (unsigned long long)q << (8 * x);
+  }
+  r.word = word;
+  r.stats = b->stats_dev;
+  static int dbg = getenv("VAD_MFCC_BALANCE_DEBUG") ? atoi(getenv("VAD_MFCC_BALANCE_DEBUG")) : 0;
+  static unsigned long long calls = 0;
+  if (dbg && (++calls % dbg) == 0) {
+    fprintf(stderr, "balance: word %016llx speeds", word);
+    for (int x = 0; x < 8; ++x) fprintf(stderr, " %.4f", sp[x]);
+    fprintf(stderr, " tiles");
+    for (int x = 0; x < 8; ++x) fprintf(stderr, " %.0f", tiles[x]);
+    fprintf(stderr, "\n");
+  }
+  return r;
+}
+}  // namespace
 
 struct vad_mfcc_plan {
   MfccDev host;      // host copy (for introspection)
@@ -25,6 +136,7 @@ struct vad_mfcc_plan {
   int fft_n;         // 512, or another length run by spec_generic.hip
   int bins;          // fft_n / 2 spectrum bins kept (mfcc.py:61)
   double2* tw_gen;   // exp(-2 pi i m / fft_n), m < fft_n (other lengths only)
+  BalanceHost* bal;  // the MFCC kernel's XCD balance (null: equal runs)
   bool generic() const { return fft_n != kFftN; }
 };
 
@@ -178,12 +290,14 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
   if (e != hipSuccess) {
     (void)hipFree(p->dev); (void)hipFree(p->hop_blob); (void)hipFree(p->tw_gen); free(p); return (int)e;
   }
+  p->bal = balance_create();
   *out = p;
   return VAD_OK;
 }
 
 int vad_mfcc_plan_destroy(vad_mfcc_plan* p) {
   if (!p) return VAD_OK;
+  balance_destroy(p->bal);
   (void)hipFree(p->dev);
   (void)hipFree(p->hop_blob);
   (void)hipFree(p->tw_gen);
@@ -245,7 +359,8 @@ int vad_mfcc_f32(const vad_mfcc_plan* p, const float* src, int64_t stride, int32
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
                                                (hipStream_t)stream);
-  return (int)launch_mfcc(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream,
+                         balance_for_launch(p->bal));
 }
 
 int vad_spec_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int32_t len, int64_t n,
@@ -263,7 +378,8 @@ int vad_mfcc_i16(const vad_mfcc_plan* p, const int16_t* src, int64_t stride, int
   if (r || n == 0) return r;
   if (p->generic()) return (int)launch_generic_i16(0, p->dev, src, stride, len, n, p->fft_n, p->tw_gen, mfcc,
                                                    (hipStream_t)stream);
-  return (int)launch_mfcc_i16(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream);
+  return (int)launch_mfcc_i16(0, p->dev, launch_spec(p), src, stride, len, n, mfcc, (hipStream_t)stream,
+                             balance_for_launch(p->bal));
 }
 
 int vad_mfcc_from_spec_f32(const vad_mfcc_plan* p, const float* spec, int64_t n, float* mfcc,
@@ -662,9 +778,11 @@ static int mfcc_ffn_entry(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, co
     VAD_TRY(launch_generic(0, plan->dev, (const float*)audio, hop, frame_size, f, plan->fft_n, plan->tw_gen, mf,
                            st));
   else if (tin_bytes == 2)
-    VAD_TRY(launch_mfcc_i16(0, plan->dev, launch_spec(plan), (const int16_t*)audio, hop, frame_size, f, mf, st));
+    VAD_TRY(launch_mfcc_i16(0, plan->dev, launch_spec(plan), (const int16_t*)audio, hop, frame_size, f, mf, st,
+                            balance_for_launch(plan->bal)));
   else
-    VAD_TRY(launch_mfcc(0, plan->dev, launch_spec(plan), (const float*)audio, hop, frame_size, f, mf, st));
+    VAD_TRY(launch_mfcc(0, plan->dev, launch_spec(plan), (const float*)audio, hop, frame_size, f, mf, st,
+                        balance_for_launch(plan->bal)));
   return (int)launch_ffn(ffn->net, 0, mf, f - 5, plan->host.mfcc_n, mode, labels, st);
 }
 

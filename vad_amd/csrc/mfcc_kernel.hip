@@ -675,7 +675,7 @@ __device__ __forceinline__ void lds_barrier() {
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0, bool WIN = false>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
-    int frame_len, int64_t n_frames, float* __restrict__ out) {
+    int frame_len, int64_t n_frames, float* __restrict__ out, MfccBalance bal) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* P = reinterpret_cast<float*>(smem);                      // [64][260] power rows
   v2f* scr = reinterpret_cast<v2f*>(smem + kPBytes);              // FFT transposes
@@ -740,10 +740,12 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
 #ifndef VAD_FRAME_RUNS
 #define VAD_FRAME_RUNS 0  // 1: frame-granular runs (A/B: C2 -1.6 %, C3 +0.7 %)
 #endif
+    // tile runs balanced over the XCDs' clocks (MfccBalance; word 0: equal)
+    const unsigned long long rt0 = bal.stats ? __builtin_amdgcn_s_memrealtime() : 0;
     const int64_t f_beg = VAD_FRAME_RUNS ? n_frames * blockIdx.x / gridDim.x
-                                         : (int64_t)blockIdx.x * n_tiles / gridDim.x * kTile;
+                                         : balanced_tile(bal.word, n_tiles, blockIdx.x, gridDim.x) * kTile;
     const int64_t f_end0 = VAD_FRAME_RUNS ? n_frames * (blockIdx.x + 1) / gridDim.x
-                                          : ((int64_t)blockIdx.x + 1) * n_tiles / gridDim.x * kTile;
+                                          : balanced_tile(bal.word, n_tiles, blockIdx.x + 1, gridDim.x) * kTile;
     const int64_t f_end = f_end0 < n_frames ? f_end0 : n_frames;
     auto pair_base = [&](int64_t t, int& lim) {
       if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
@@ -895,6 +897,10 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       if (prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
         phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
     }
+    // this run's speed for the host's next balance (runs of >= 8 tiles only:
+    // shorter ones are mostly launch ramp)
+    if (bal.stats && tid == 0 && t_end >= 8)
+      bal.stats[blockIdx.x] = ((unsigned long long)t_end << 40) | (__builtin_amdgcn_s_memrealtime() - rt0);
     if constexpr (DIAG == 9) {
       __syncthreads();
       if (tid == 0) {
@@ -1691,7 +1697,7 @@ static int num_cus() {
 template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0,
           int HOPC = 0, bool WIN = false>
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
-                           int64_t n, float* out, hipStream_t st) {
+                           int64_t n, float* out, hipStream_t st, const MfccBalance& bal = MfccBalance()) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
   const int cap = num_cus();  // persistent, LDS-bound: one workgroup per CU
   const int grid = (int)(n_tiles < cap ? n_tiles : cap);
@@ -1702,13 +1708,13 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
       attr_done);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC, WIN>), dim3(grid), dim3(kThreads),
-                     smem, st, plan, src, stride, len, n, out);
+                     smem, st, plan, src, stride, len, n, out, bal);
   return hipGetLastError();
 }
 
 template <typename TIN, int MODE>
 static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_t stride, int len,
-                           int64_t n, float* out, hipStream_t st) {
+                           int64_t n, float* out, hipStream_t st, const MfccBalance& bal = MfccBalance()) {
   const int used = len < kFftN ? len : kFftN;
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
                     ((stride & 1) == 0) && ((used & 1) == 0);
@@ -1717,9 +1723,9 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
     // optional analysis window at the reference framing: the paired-frame
     // kernel with the window applied in its stage A (and the generated mel
     // code when the bank is a compiled one)
-    if (spec == kSpecWindow26) return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5, true>(plan, src, stride, len, n, out, st);
-    if (spec == kSpecWindow40) return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5, true>(plan, src, stride, len, n, out, st);
-    return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5, true>(plan, src, stride, len, n, out, st);
+    if (spec == kSpecWindow26) return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
+    if (spec == kSpecWindow40) return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
+    return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
   }
   if (spec == kSpecWindow26 || spec == kSpecWindow40) spec = kSpecWindow;
   if (spec == kSpecWindow) {  // optional analysis window: the runtime-table kernel with WIN
@@ -1741,18 +1747,18 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
       if (stride == 160 && kPairFrames && VAD_MFCC3)  // the reference hop (config.py:22): 3 waves / SIMD
         return launch_mfcc3<TIN, 1>(plan, src, n, out, st);
       if (stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st);
+        return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2) {
       if (stride == 160 && kPairFrames && VAD_MFCC3)
         return launch_mfcc3<TIN, 2>(plan, src, n, out, st);
       if (stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5>(plan, src, stride, len, n, out, st);
+        return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
     }
     if (stride == 160 && kPairFrames)
-      return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5>(plan, src, stride, len, n, out, st);
+      return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5>(plan, src, stride, len, n, out, st, bal);
     return launch_t<TIN, MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
   }
   if (used <= 32 * 13) {
@@ -1764,10 +1770,10 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
 }
 
 hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
-                       int len, int64_t n, float* out, hipStream_t st) {
+                       int len, int64_t n, float* out, hipStream_t st, const MfccBalance& bal) {
   if (n <= 0) return hipSuccess;
   switch (mode) {
-    case kAudioToMfcc: return launch_m<float, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
+    case kAudioToMfcc: return launch_m<float, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st, bal);
     case kAudioToSpec:
       return launch_m<float, kAudioToSpec>(plan, spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40
                                                      ? kSpecWindow : 0, src, stride, len, n, out, st);
@@ -1783,12 +1789,12 @@ hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src
 }
 
 hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_t* src,
-                           int64_t stride, int len, int64_t n, float* out, hipStream_t st) {
+                           int64_t stride, int len, int64_t n, float* out, hipStream_t st, const MfccBalance& bal) {
   if (n <= 0) return hipSuccess;
   if (mode == kAudioToSpec)
     return launch_m<int16_t, kAudioToSpec>(plan, spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40
                                                        ? kSpecWindow : 0, src, stride, len, n, out, st);
-  return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st);
+  return launch_m<int16_t, kAudioToMfcc>(plan, spec, src, stride, len, n, out, st, bal);
 }
 
 // Fused clip entry (vad_mfcc_ffn): the reference framing (400 / 160), the

@@ -93,12 +93,41 @@ struct TreeNodeC {
   int right;
 };
 
+// XCD-balanced tile runs of the persistent MFCC kernel (paired-frame path).
+// The 8 XCDs of an MI355X run at their own shader clocks under load (one
+// box: 2.04-2.26 GHz), while every workgroup of an equal split does the
+// same number of cycles, so the slowest XCD sets the launch time.  `word`
+// holds 8 weights (8 bits each, >= 1; 0 = equal split): workgroup b's
+// share of the tiles is proportional to the weight of b mod 8 (the XCD
+// the dispatcher deals it to; a different placement costs balance, never
+// correctness: the runs always partition the tiles exactly).  `stats`
+// (host-mapped, may be null): per workgroup (tiles << 40) | s_memrealtime
+// ticks, from which the host derives the next launch's weights.
+struct MfccBalance {
+  unsigned long long word = 0;
+  unsigned long long* stats = nullptr;
+};
+// first tile of workgroup b's run (b = G: n_tiles)
+__host__ __device__ inline int64_t balanced_tile(unsigned long long word, int64_t n_tiles, int b, int G) {
+  if (word == 0) return (int64_t)b * n_tiles / G;
+  int64_t w8 = 0, part = 0;
+  for (int x = 0; x < 8; ++x) {
+    const int64_t w = (int64_t)((word >> (8 * x)) & 255u);
+    w8 += w;
+    part += x < (b & 7) ? w : 0;
+  }
+  int64_t tot = (int64_t)(G >> 3) * w8;
+  for (int x = 0; x < (G & 7); ++x) tot += (int64_t)((word >> (8 * x)) & 255u);
+  return n_tiles * ((int64_t)(b >> 3) * w8 + part) / tot;
+}
+
 // Launchers (defined in the .hip translation units).
 size_t mfcc_smem_bytes();
 hipError_t launch_mfcc(int mode, const MfccDev* plan, int spec, const float* src, int64_t stride,
-                       int len, int64_t n, float* out, hipStream_t st);
+                       int len, int64_t n, float* out, hipStream_t st, const MfccBalance& bal = MfccBalance());
 hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_t* src,
-                           int64_t stride, int len, int64_t n, float* out, hipStream_t st);
+                           int64_t stride, int len, int64_t n, float* out, hipStream_t st,
+                           const MfccBalance& bal = MfccBalance());
 bool mfcc_ffn_fusable(int spec, const FfnDev& net, int frame_size, int hop, const void* audio, int tin_bytes);
 hipError_t launch_mfcc_ffn(const MfccDev* plan, const FfnDev& net, const void* audio, int tin_bytes,
                            int64_t n_frames, int mode, uint8_t* labels, hipStream_t st);
