@@ -340,7 +340,10 @@ struct WaveResidency {
   static constexpr bool kAll = VAD_FFN_ALL_LDS != 0 && KS0 == 4 && NC <= 2;
   static constexpr bool kLdsFrags = KS0 == 10 || NC > 2 || kAll;
   static constexpr bool kLdsSlots = (VAD_FFN_LDS_SLOTS != 0 && !kLdsFrags) || kAll;
-  static constexpr int kWavesPerSimd = kAll ? 4 : KS0 == 10 ? 3 : kLdsSlots ? 3 : 2;
+#ifndef VAD_FFN_ALL_WPS
+#define VAD_FFN_ALL_WPS 4
+#endif
+  static constexpr int kWavesPerSimd = kAll ? VAD_FFN_ALL_WPS : KS0 == 10 ? 3 : kLdsSlots ? 3 : 2;
 };
 // Fragments with the hi halves (and layer 0's lo halves) in VGPRs and the lo
 // halves of slots >= LO_FROM read from a workgroup-shared LDS copy
@@ -366,8 +369,12 @@ struct LdsRow {
 constexpr int kWRows = (kWTile + 4) * 13;        // staged MFCC floats per tile (260)
 constexpr int kWRowRegs = (kWRows + 63) / 64;    // 5 per lane
 
+#ifndef VAD_FFN_WPB
+#define VAD_FFN_WPB 4  // waves per block (sharing one LDS fragment copy)
+#endif
+constexpr int kWpb = VAD_FFN_WPB;
 template <int KS0, int T1, int T2, int T3, int T4, int NC, int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResidency<KS0, NC>::kWavesPerSimd))) void ffn_wave_kernel(
+__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveResidency<KS0, NC>::kWavesPerSimd))) void ffn_wave_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
   // VAD_FFN_WAVE_MFMA_OUT: the output layer on the MFMA too (the plan's
   // fragh holds its slots after the hidden layers'); default: bl13's on the
@@ -378,9 +385,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
   static_assert(KS0 == 4 || KS0 == 10, "specialised topologies: 13 or 39 inputs");
   constexpr int IN = KS0 == 4 ? MN : 3 * MN;  // network inputs (features 0 .. IN-1)
   constexpr int XS = 32 * HP::K0 + 4;         // floats per feature row: 16-B aligned
-  __shared__ float rows_s[4][kWRows];
-  __shared__ __attribute__((aligned(16))) float x_s[4][kWTile * XS];
-  __shared__ int flat_s[4][kWTile];  // per window: some coefficient is flat (NaN features)
+  __shared__ float rows_s[kWpb][kWRows];
+  __shared__ __attribute__((aligned(16))) float x_s[kWpb][kWTile * XS];
+  __shared__ int flat_s[kWpb][kWTile];  // per window: some coefficient is flat (NaN features)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   const int g = lane >> 4;
@@ -406,7 +413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
   if constexpr (kLdsSlots) {
     // slot sl of lane group gg (the host's fragment order: biases, then the
     // VALU layer's class slots, then its biases after 4 classes' worth)
-    for (int i = threadIdx.x; i < 4 * NSLP; i += 256) {
+    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kWpb) {
       const int gg = i / NSLP, sl = i - gg * NSLP;
       const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
                                      : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
@@ -414,7 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
       slot_s[i] = sl < NSL ? net.frag[src_sl * 64 + 16 * gg] : 0.f;
     }
     // the lo halves of the layers after the first: [slot - S0][lane]
-    for (int i = threadIdx.x; i < kLoSlots * 64; i += 256)
+    for (int i = threadIdx.x; i < kLoSlots * 64; i += 64 * kWpb)
       fhlo_s[i] = reinterpret_cast<const u4*>(net.fragh)[(2 * (kLoFrom + i / 64) + 1) * 64 + (i & 63)];
     __syncthreads();
   } else {
@@ -431,7 +438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
   __shared__ u4 fh_s[kLdsFrags ? HP::NS * 2 * 64 : 1];
   u4 fh_r[kLdsFrags ? 1 : HP::NS][2];
   if constexpr (kLdsFrags) {
-    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 256) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
+    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 64 * kWpb) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
     __syncthreads();
   } else {
     load_fragh<HP>(net.fragh, lane, *reinterpret_cast<u4(*)[HP::NS][2]>(fh_r));
@@ -446,8 +453,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WaveResiden
 
   const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
   const int64_t total = (n_rows + 4) * MN;  // MFCC floats the windows can read
-  const int64_t wave_id = (int64_t)blockIdx.x * 4 + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * 4;
+  const int64_t wave_id = (int64_t)blockIdx.x * kWpb + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * kWpb;
   // branch-free and select-free (a select on the loaded value would make the
   // prefetch wait at the loop's back edge): offsets past the rows clamp to
   // the last float, so the last tile's unused windows see finite rows.  The
@@ -614,15 +621,15 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
     if constexpr (kH3) {
       if (mfcc_n == 13 && net.fragh && VAD_FFN_WAVE) {
         // one resident wave per SIMD pair slot: 2 blocks of 4 waves per CU
-        int64_t wblocks = (n_rows + 4 * kWTile - 1) / (4 * kWTile);
-        const int64_t wcap = WaveResidency<KS0, NC>::kWavesPerSimd * ffn_num_cus();
+        int64_t wblocks = (n_rows + kWpb * kWTile - 1) / (kWpb * kWTile);
+        const int64_t wcap = WaveResidency<KS0, NC>::kWavesPerSimd * 4 / kWpb * ffn_num_cus();
         if (wblocks > wcap) wblocks = wcap;
         if (mode == VAD_FEAT_OFFLINE)
           hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE>),
-                             dim3((int)wblocks), dim3(256), 0, st, net, in, n_rows, labels);
+                             dim3((int)wblocks), dim3(64 * kWpb), 0, st, net, in, n_rows, labels);
         else
           hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_ANALYSER>),
-                             dim3((int)wblocks), dim3(256), 0, st, net, in, n_rows, labels);
+                             dim3((int)wblocks), dim3(64 * kWpb), 0, st, net, in, n_rows, labels);
         return hipGetLastError();
       }
       if (mfcc_n == 13 && net.fragh) {
