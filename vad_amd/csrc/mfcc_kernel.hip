@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // MFCC rows, in a buffer the caller over-allocates; outputs stay exact
     unsigned long long* wg_st = reinterpret_cast<unsigned long long*>(out + n_frames * 13) + blockIdx.x * 4;
     (void)wg_st;
-    if constexpr (DIAG == 9) {
+    if constexpr (DIAG == 9 || DIAG == 10) {  // per-workgroup start / end (tools/wgtime.py)
       if (tid == 0) {
         wg_st[0] = __builtin_amdgcn_s_memtime();
         wg_st[1] = __builtin_amdgcn_s_memrealtime();
@@ -901,7 +901,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // shorter ones are mostly launch ramp)
     if (bal.stats && tid == 0 && t_end >= 8)
       bal.stats[blockIdx.x] = ((unsigned long long)t_end << 40) | (__builtin_amdgcn_s_memrealtime() - rt0);
-    if constexpr (DIAG == 9) {
+    if constexpr (DIAG == 9 || DIAG == 10) {  // per-workgroup start / end (tools/wgtime.py)
       __syncthreads();
       if (tid == 0) {
         wg_st[2] = __builtin_amdgcn_s_memtime();
