@@ -462,7 +462,8 @@ def main():
                   "collective": "gather" if gathers[0].use_gather else "all_gather",
                   "backend": args.backend, "gathers_timed": n_g,
                   "note": "standalone (host-timed, max over ranks); in the timed steps each gather "
-                          "overlaps the next step's kernels on RCCL's stream"}
+                          + ("overlaps the next step's kernels on RCCL's stream" if args.backend == "nccl"
+                             else "runs through gloo's host path (rehearsal backend)")}
     mfcc_ms, mfcc_pct = kernel_ms(lambda: pipe.mfcc(audio, out=mfcc))
     ffn_ms, ffn_pct = kernel_ms(lambda: ffn_plan.window_labels(mfcc, out=labels))
     # the fused single-kernel clip form (MFCC rows kept on chip) and the FFN
