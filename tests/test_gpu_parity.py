@@ -511,6 +511,48 @@ def test_stream_hop_blocks_equal_single_hops(torch_cuda, golden, kernel, K):
     assert (want[:5] == 255).all() and (want[5:] != 255).all()
 
 
+@pytest.mark.parametrize("frame_size,hop", [(512, 256), (1000, 400)])
+def test_stream_hop_long_frames(torch_cuda, golden, frame_size, hop):
+    """Frames longer than 448 samples take the hop kernel's 16-chunk build
+    (stream_kernel.hip, NR = 16; 1000 samples: the FFT truncates to 512, as
+    np.fft.fft(x, 512) does): its MFCC ring matches the three-kernel form's
+    (the clip MFCC kernel on the same frames) to 1e-4 per row, blocks of
+    hops equal single hops, and the labels agree wherever both rings do."""
+    import torch
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    cfg = MfccConfig(frame_size=frame_size, hop=hop)
+    S, T, K = 5, 16, 4
+    carry_n = frame_size - hop
+    clips = [O.synth_clip(hop * T + carry_n, seed=900 + s) for s in range(S)]
+    carry = torch.from_numpy(np.stack([c[:carry_n] for c in clips])).cuda()
+    hops = torch.from_numpy(np.ascontiguousarray(np.stack(
+        [np.stack([c[carry_n + hop * t: carry_n + hop * (t + 1)] for c in clips]) for t in range(T)]))).cuda()
+    three = StreamBatch(S, clf, cfg=cfg, kernel="three")
+    one = StreamBatch(S, clf, cfg=cfg, kernel="hop")
+    three.prime(carry)
+    one.prime(carry)
+    lab3, lab1 = [], []
+    for t in range(T):
+        lab3.append(three.step(hops[t]).clone())
+        lab1.append(one.step(hops[t]).clone())
+        a, b = one.ring.double().cpu().numpy(), three.ring.double().cpu().numpy()
+        rel = np.linalg.norm(a - b, axis=2) / np.maximum(np.linalg.norm(b, axis=2), 1e-30)
+        assert rel.max() <= 1e-4, (t, rel.max())
+    assert torch.equal(one.frames, three.frames)
+    assert torch.equal(one.count, three.count)
+    blk = StreamBatch(S, clf, cfg=cfg, kernel="hop", hops_per_step=K)
+    blk.prime(carry)
+    got = torch.cat([blk.step_block(hops[b * K:(b + 1) * K]).clone() for b in range(T // K)])
+    assert torch.equal(got, torch.stack(lab1))
+    assert torch.equal(blk.ring, one.ring) and torch.equal(blk.frames, one.frames)
+    same = (torch.stack(lab1) == torch.stack(lab3)).float().mean().item()
+    assert same >= 0.9, same
+
+
 def test_stream_hop_rejects_window(torch_cuda):
     """An analysis-window plan cannot run the one-kernel hop (its table blob
     has no window): StreamBatch refuses it, and so does the C ABI."""
