@@ -66,6 +66,7 @@ BalanceHost* balance_create() {
 
 void balance_destroy(BalanceHost* b) {
   if (!b) return;
+  (void)hipDeviceSynchronize();  // no launch of this plan may still write its stats
   (void)hipHostFree(b->stats_host);
   delete b;
 }
