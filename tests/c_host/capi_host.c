@@ -8,8 +8,9 @@
  *                      <dir>/mfcc_ref.f32 (the oracle's MFCCs, F x 13),
  *                      <dir>/ffn.f32 + <dir>/labels_ref.u8 (13-64-64-2
  *                      weights, oracle labels where decisive, 255 elsewhere)
- * and checks vad_mfcc_f32, vad_mfcc_ffn (workspace and fused forms) and a
- * world-size-1 vad_rccl gather.  Exit status 0 = all checks passed.
+ * and checks vad_mfcc_f32, vad_mfcc_ffn (workspace and fused forms), the
+ * clip as one stream through vad_stream_hops, and a world-size-1 vad_rccl
+ * gather.  Exit status 0 = all checks passed.
  */
 #include <hip/hip_runtime_api.h>
 #include <math.h>
@@ -111,6 +112,49 @@ int main(int argc, char** argv) {
     }
   }
   printf("labels: %zu windows, %zu decisive ones equal the oracle, fused == two-kernel\n", nl, checked);
+
+  /* the streaming form (vad.py:32-59's loop, sklearn_analyser.py:46-82 per
+   * hop): the clip as one live stream, 8 hops of 160 new samples per
+   * vad_stream_hops call, read in place from the clip; hop t's label is the
+   * class of clip window t - 5 (255 for the first five hops) */
+  {
+    const int K = 8;
+    const int64_t T = (F / K) * K;
+    float *d_frames, *d_ring;
+    int32_t* d_count;
+    uint8_t* d_hl;
+    CHECK(hipMalloc((void**)&d_frames, 400 * 4));
+    CHECK(hipMalloc((void**)&d_ring, 5 * 13 * 4));
+    CHECK(hipMalloc((void**)&d_count, 4));
+    CHECK(hipMalloc((void**)&d_hl, (size_t)T));
+    CHECK(hipMemset(d_frames, 0, 400 * 4));
+    CHECK(hipMemcpy(d_frames + 160, d_audio, 240 * 4, hipMemcpyDeviceToDevice));  /* the carry */
+    CHECK(hipMemset(d_ring, 0, 5 * 13 * 4));
+    CHECK(hipMemset(d_count, 0, 4));
+    for (int64_t b = 0; b < T / K; ++b)
+      CHECK(vad_stream_hops(plan, ffn, d_frames, 400, 400, d_audio + 240 + 160 * K * b, 160, 160, 1, K, 160,
+                            d_ring, d_count, d_hl + K * b, 1, NULL));
+    uint8_t* hl = (uint8_t*)malloc((size_t)T);
+    CHECK(hipMemcpy(hl, d_hl, (size_t)T, hipMemcpyDeviceToHost));
+    size_t hchecked = 0;
+    for (int64_t t = 0; t < T; ++t) {
+      if (t < 5) {
+        if (hl[t] != 255) { fprintf(stderr, "hop %lld: %d before the window fills\n", (long long)t, hl[t]); return 10; }
+      } else if (lref[t - 5] != 255) {
+        ++hchecked;
+        if (hl[t] != lref[t - 5]) {
+          fprintf(stderr, "hop %lld: %d vs oracle %d\n", (long long)t, hl[t], lref[t - 5]);
+          return 11;
+        }
+      }
+    }
+    printf("stream: %lld hops in blocks of %d, %zu decisive labels equal the oracle\n", (long long)T, K, hchecked);
+    free(hl);
+    CHECK(hipFree(d_frames));
+    CHECK(hipFree(d_ring));
+    CHECK(hipFree(d_count));
+    CHECK(hipFree(d_hl));
+  }
 
   /* the multi-GPU label gather, a group of one */
   if (vad_rccl_available()) {

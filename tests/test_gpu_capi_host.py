@@ -1,7 +1,8 @@
 """A non-Python host on the C ABI: tests/c_host/capi_host (plain C against
 include/vad_amd.h, built on the CPU by ``vad_amd.build.build_c_host``) reads
 oracle-made inputs from files and checks vad_mfcc_f32, vad_mfcc_ffn (both
-clip forms) and a world-size-1 vad_rccl gather, the way a cgo / JNI binding of
+clip forms), the clip as one stream through vad_stream_hops (8 hops per call)
+and a world-size-1 vad_rccl gather, the way a cgo / JNI binding of
 the reference's path (mfcc.py:67-78, sklearn_analyser.py:46-82) would call
 them.  It runs as a child process, so it owns its own HIP context."""
 import os
