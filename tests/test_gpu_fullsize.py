@@ -205,3 +205,37 @@ def test_split_f16_logit_error_bounded(torch_cuda, topo):
     print(f"logit error / max|logit|: split-f16 {err['split_f16']:.3e}, exact f32 {err['f32']:.3e}")
     assert err["f32"] < 1e-5
     assert err["split_f16"] <= SPLIT_VS_F32 * err["f32"], err
+
+
+def test_clip_past_2g_samples(torch_cuda):
+    """Maximum-size edge: a 14M-frame clip (2.24e9 samples, 9 GB of fp32 and
+    4.5 GB of int16 on the device) takes sample offsets past 2^31 and byte
+    offsets past 2^32.  Every frame's computation is position independent,
+    so windows of the big clip, at its start, across sample 2^31 and at its
+    end, equal (bit for bit) the same frames cut out as small clips: MFCCs
+    (fp32 and int16 input) and the two-kernel labels.  Size-independent
+    property check: the oracle stays at the small sizes of the other tests."""
+    torch = torch_cuda
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    free, _ = torch.cuda.mem_get_info()
+    if free < 24 << 30:
+        pytest.skip("needs ~24 GB of free device memory")
+    F = 14_000_000
+    n = 160 * (F - 1) + 401
+    assert n > 2 ** 31
+    g = torch.Generator(device="cuda").manual_seed(77)
+    audio = (torch.randn(n, generator=g, device="cuda") * 3000).round_().clamp_(-32767, 32767)
+    pipe = VadPipeline(FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)))
+    big = pipe.mfcc(audio)
+    big_lab = pipe.labels(audio)
+    a16 = audio.to(torch.int16)
+    assert torch.equal(pipe.mfcc(a16), big)
+    del a16
+    W = 2000  # frames per cut
+    for f0 in (0, (2 ** 31) // 160 - W // 2, F - W):
+        cut = audio[160 * f0: 160 * (f0 + W - 1) + 401].contiguous()
+        assert torch.equal(pipe.mfcc(cut), big[f0:f0 + W]), f0
+        assert torch.equal(pipe.labels(cut), big_lab[f0:f0 + W - 5]), f0
+    del audio, big, big_lab
+    torch.cuda.empty_cache()
