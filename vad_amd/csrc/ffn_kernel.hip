@@ -495,7 +495,10 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   // 128-VGPR budget a second prefetch set would spill), each with its own
   // prefetch registers (no copies at the back edge): a tile's rows are
   // loaded kPF tiles ahead
-  constexpr int kPF = WaveResidency<KS0, NC>::kAll ? 1 : VAD_FFN_PF;
+#ifndef VAD_FFN_PF_ALL
+#define VAD_FFN_PF_ALL 1
+#endif
+  constexpr int kPF = WaveResidency<KS0, NC>::kAll ? VAD_FFN_PF_ALL : VAD_FFN_PF;
   float pre[kPF][kWRowRegs];
 #pragma unroll
   for (int k = 0; k < kPF; ++k) {
