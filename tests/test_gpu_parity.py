@@ -511,20 +511,21 @@ def test_stream_hop_blocks_equal_single_hops(torch_cuda, golden, kernel, K):
     assert (want[:5] == 255).all() and (want[5:] != 255).all()
 
 
-@pytest.mark.parametrize("frame_size,hop", [(512, 256), (1000, 400)])
-def test_stream_hop_long_frames(torch_cuda, golden, frame_size, hop):
+@pytest.mark.parametrize("frame_size,hop,nf", [(512, 256, 26), (1000, 400, 26), (400, 160, 40)])
+def test_stream_hop_long_frames(torch_cuda, golden, frame_size, hop, nf):
     """Frames longer than 448 samples take the hop kernel's 16-chunk build
     (stream_kernel.hip, NR = 16; 1000 samples: the FFT truncates to 512, as
-    np.fft.fft(x, 512) does): its MFCC ring matches the three-kernel form's
-    (the clip MFCC kernel on the same frames) to 1e-4 per row, blocks of
-    hops equal single hops, and the labels agree wherever both rings do."""
+    np.fft.fft(x, 512) does), and 40 filters take 40 mel lanes: the MFCC
+    ring matches the three-kernel form's (the clip MFCC kernel on the same
+    frames) to 1e-4 per row, blocks of hops equal single hops, and the
+    labels agree wherever both rings do."""
     import torch
     from vad_amd.config import MfccConfig
     from vad_amd.ffn import FFNClassifier
     from vad_amd.stream import StreamBatch
     w = golden("ffn")
     clf = FFNClassifier(layers_from(w, "ref39", 4))
-    cfg = MfccConfig(frame_size=frame_size, hop=hop)
+    cfg = MfccConfig(frame_size=frame_size, hop=hop, n_filters=nf)
     S, T, K = 5, 16, 4
     carry_n = frame_size - hop
     clips = [O.synth_clip(hop * T + carry_n, seed=900 + s) for s in range(S)]
