@@ -157,6 +157,33 @@ def test_analyser_rows_match_reference_run(torch_cuda, golden, tmp_path, key):
     check_rows(got, ref, win, f"analyser rows ({key})")
 
 
+@pytest.mark.parametrize("fbank_num,low_hz,high_hz", [(40, 300, 8000), (20, 100, 7000)])
+def test_analyser_rows_other_banks_vs_oracle(torch_cuda, golden, tmp_path, fbank_num, low_hz, high_hz):
+    """The analyser's constructor parameters beyond the reference defaults
+    (sklearn_analyser.py:16-33: fbank_num, low_hz, high_hz): the compiled
+    40-filter bank and a runtime-table bank (20 filters, 100-7000 Hz), rows
+    passed to predict vs the oracle's rows of the oracle's fp64 MFCCs on the
+    fixture stream (parity pinned through the oracle's filterbank and MFCC
+    fixtures; the reference run covers the 26-filter default only)."""
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    g = golden("analyser")
+    frames = list(g["stream"])
+    p = tmp_path / "rec.pkl"
+    with open(p, "wb") as f:
+        pickle.dump(FeatureRecorder([0] * len(frames)), f)
+    an = SKLearnAnalyzer(str(p), low_hz=low_hz, high_hz=high_hz, fbank_num=fbank_num)
+    an.load_init_inactive_frames(list(g["noise"]))
+    for fr in frames:
+        an.feed_frame(fr)
+    got = np.concatenate(an.classifier.rows)
+    fb = O.get_mel_filterbanks(low_hz, high_hz, 512, fbank_num, 16000)
+    mfcc = np.stack([O.get_mfcc(fr, 512, fb, 13) for fr in frames])
+    win = windows(mfcc)
+    ref = np.where(flat_nan_mask(win), np.nan, O.analyser_features(mfcc))
+    assert got.shape == ref.shape == (len(frames) - 5, 39)
+    check_rows(got, ref, win, f"analyser rows ({fbank_num} filters, {low_hz}-{high_hz} Hz)")
+
+
 def test_c3_clip_features_vs_oracle(torch_cuda):
     """C3 size (1M frames): the device's analyser window features vs the
     oracle's features of the oracle's fp64 MFCCs, NaN positions exact (flat
