@@ -827,3 +827,50 @@ def test_other_fft_length_pipeline(torch_cuda):
     hop.prime(torch.from_numpy(np.stack([clip[:240]] * 3)).cuda())
     with pytest.raises(RuntimeError):
         hop.step(torch.from_numpy(np.stack([clip[240:400]] * 3)).cuda())
+
+
+@pytest.mark.parametrize("mfcc_n", [1, 12, 16])
+def test_other_coefficient_counts(torch_cuda, mfcc_n):
+    """get_mfcc's mfcc_n (mfcc.py:67-78; the analyser's mfcc_num) other than
+    13, up to VAD_MAX_MFCC: the runtime-table kernel's lifter x DCT rows,
+    the analyser window features (3 mfcc_n columns) and a generic-topology
+    FFN on them, the clip path and the one-kernel hop, vs the oracle."""
+    import torch
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.plan import window_features
+    from vad_amd.stream import StreamBatch
+    cfg = MfccConfig(n_mfcc=mfcc_n)
+    F = 3000
+    clip = O.synth_clip(O.samples_for_frames(F), seed=41)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    ref = O.mfcc_batch(clip, fb, mfcc_n=mfcc_n)
+    layers = random_layers((3 * mfcc_n, 32, 2), seed=9)
+    pipe = VadPipeline(FFNClassifier(layers), cfg=cfg)
+    a = torch.from_numpy(clip).cuda()
+    m = pipe.mfcc(a)
+    got = m.cpu().numpy().astype(np.float64)
+    assert got.shape == ref.shape == (F, mfcc_n)
+    # norm-wise per frame (SURVEY 8(c)) against the frame's 13-coefficient
+    # norm at least: with one coefficient, c0 alone can sit near 0
+    ref13 = O.mfcc_batch(clip, fb)
+    den = np.maximum(np.linalg.norm(ref, axis=1), np.linalg.norm(ref13, axis=1))
+    rel = np.linalg.norm(got - ref, axis=1) / den
+    assert rel.max() <= 1e-4, rel.max()
+    x = O.analyser_features_fast(ref)
+    feats = window_features(m).cpu().numpy()
+    assert feats.shape == x.shape == (F - 5, 3 * mfcc_n)
+    labels = pipe.labels(a).cpu().numpy()
+    sure = O.ffn_margin(x, layers) > MARGIN_TOL
+    np.testing.assert_array_equal(labels[sure], O.ffn_labels(x, layers)[sure])
+    # the streaming hop on the same frames: its window labels agree where decisive
+    T = 64
+    sb = StreamBatch(2, FFNClassifier(layers), cfg=cfg, kernel="hop")
+    sb.prime(torch.from_numpy(np.stack([clip[:240]] * 2)).cuda())
+    hl = np.stack([sb.step(torch.from_numpy(np.stack([clip[240 + 160 * t: 400 + 160 * t]] * 2)).cuda())
+                   .cpu().numpy().copy() for t in range(T)])
+    assert (hl[:5] == 255).all()
+    ok = sure[:T - 5]
+    np.testing.assert_array_equal(hl[5:, 0][ok], O.ffn_labels(x, layers)[:T - 5][ok])
+    np.testing.assert_array_equal(hl[:, 0], hl[:, 1])
