@@ -874,3 +874,22 @@ def test_other_coefficient_counts(torch_cuda, mfcc_n):
     ok = sure[:T - 5]
     np.testing.assert_array_equal(hl[5:, 0][ok], O.ffn_labels(x, layers)[:T - 5][ok])
     np.testing.assert_array_equal(hl[:, 0], hl[:, 1])
+
+
+def test_other_sample_rate(torch_cuda):
+    """An 8 kHz configuration (get_mel_filterbanks' sample_rate, mfcc.py:39-56;
+    the analyser's sample_rate): 20 ms frames, 10 ms hop, 256-point FFT,
+    26 filters up to 4 kHz -- the runtime-table / generic-FFT path, MFCCs
+    vs the oracle norm-wise per frame."""
+    import torch
+    from vad_amd.config import MfccConfig
+    from vad_amd.pipeline import VadPipeline
+    cfg = MfccConfig(sample_rate=8000, frame_size=160, hop=80, fft_n=256, low_hz=300, high_hz=4000)
+    F = 2000
+    clip = O.synth_clip(80 * (F - 1) + 161, seed=43)
+    fb = O.get_mel_filterbanks(300, 4000, 256, 26, 8000)
+    ref = O.mfcc_batch(clip, fb, frame_size=160, step=80, fft_n=256)
+    got = VadPipeline(cfg=cfg).mfcc(torch.from_numpy(clip).cuda()).cpu().numpy().astype(np.float64)
+    assert got.shape == ref.shape == (F, 13)
+    rel = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
+    assert rel.max() <= 1e-4, rel.max()
