@@ -1690,6 +1690,14 @@ static int num_cus() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
+#if VAD_DIAG_BUILD != 0
+    // diagnostic libraries only: VAD_MFCC_CUS=n runs the persistent grid on
+    // fewer workgroups (clock-versus-load experiments, tools/wgtime.py)
+    if (const char* e = getenv("VAD_MFCC_CUS")) {
+      const int k = atoi(e);
+      if (k > 0 && k < n) n = k;
+    }
+#endif
   }
   return n;
 }
