@@ -893,3 +893,41 @@ def test_other_sample_rate(torch_cuda):
     assert got.shape == ref.shape == (F, 13)
     rel = np.linalg.norm(got - ref, axis=1) / np.linalg.norm(ref, axis=1)
     assert rel.max() <= 1e-4, rel.max()
+
+
+def test_nonfinite_samples(torch_cuda):
+    """Corrupted audio: a NaN and an inf sample.  The reference's float path
+    (mfcc.py:59-78) turns every frame that contains one into a NaN MFCC row
+    (np.fft spreads it over every bin) and its windows into NaN feature rows,
+    which the Keras forward keeps NaN and np.argmax maps to class 0; frames
+    without one are untouched.  The device gives the same NaN rows (fp32 and
+    int16-free path), finite rows within the usual tolerance elsewhere, and
+    class 0 on every window that sees a NaN row."""
+    import torch
+    from vad_amd.ffn import FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 400
+    clip = O.synth_clip(O.samples_for_frames(F), seed=47).astype(np.float32)
+    clip[160 * 100 + 7] = np.nan
+    clip[160 * 300 + 200] = np.inf
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    with np.errstate(invalid="ignore", over="ignore"):
+        ref = O.mfcc_batch(clip, fb)
+    layers = random_layers((13, 64, 64, 2), seed=3)
+    pipe = VadPipeline(FFNClassifier(layers))
+    a = torch.from_numpy(clip).cuda()
+    got = pipe.mfcc(a).cpu().numpy().astype(np.float64)
+    bad_ref = ~np.isfinite(ref).all(axis=1)
+    bad_got = ~np.isfinite(got).all(axis=1)
+    assert bad_ref.any()
+    np.testing.assert_array_equal(bad_got, bad_ref)
+    ok = ~bad_ref
+    rel = np.linalg.norm(got[ok] - ref[ok], axis=1) / np.linalg.norm(ref[ok], axis=1)
+    assert rel.max() <= 1e-4
+    labels = pipe.labels(a).cpu().numpy()
+    win_bad = np.array([bad_ref[i:i + 5].any() for i in range(F - 5)])
+    assert (labels[win_bad] == 0).all()
+    with np.errstate(invalid="ignore"):
+        x = O.analyser_features_fast(ref)[:, :13]
+        sure = O.ffn_margin(x, layers) > MARGIN_TOL
+    np.testing.assert_array_equal(labels[sure & ~win_bad], O.ffn_labels(x, layers)[sure & ~win_bad])
