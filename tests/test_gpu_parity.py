@@ -900,9 +900,10 @@ def test_nonfinite_samples(torch_cuda):
     (mfcc.py:59-78) turns every frame that contains one into a NaN MFCC row
     (np.fft spreads it over every bin) and its windows into NaN feature rows,
     which the Keras forward keeps NaN and np.argmax maps to class 0; frames
-    without one are untouched.  The device gives the same NaN rows (fp32 and
-    int16-free path), finite rows within the usual tolerance elsewhere, and
-    class 0 on every window that sees a NaN row."""
+    without one are untouched.  The device gives the same NaN rows, finite
+    rows within the usual tolerance elsewhere, and class 0 on every window
+    that sees a NaN row -- in the two-kernel clip form, the fused kernel and
+    the one-kernel streaming hop."""
     import torch
     from vad_amd.ffn import FFNClassifier, random_layers
     from vad_amd.pipeline import VadPipeline
@@ -927,6 +928,15 @@ def test_nonfinite_samples(torch_cuda):
     labels = pipe.labels(a).cpu().numpy()
     win_bad = np.array([bad_ref[i:i + 5].any() for i in range(F - 5)])
     assert (labels[win_bad] == 0).all()
+    # the fused kernel and the one-kernel streaming hop on the same samples
+    np.testing.assert_array_equal(pipe.labels(a, fused=True).cpu().numpy(), labels)
+    from vad_amd.stream import StreamBatch
+    sb = StreamBatch(1, FFNClassifier(layers), kernel="hop")
+    sb.prime(a[:240].reshape(1, 240))
+    hl = np.array([int(sb.step(a[240 + 160 * t: 400 + 160 * t].reshape(1, 160).contiguous())[0])
+                   for t in range(F)])
+    assert (hl[:5] == 255).all()
+    assert (hl[5:][win_bad] == 0).all()
     with np.errstate(invalid="ignore"):
         x = O.analyser_features_fast(ref)[:, :13]
         sure = O.ffn_margin(x, layers) > MARGIN_TOL
