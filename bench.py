@@ -6,8 +6,12 @@ MFCC (HIP kernel) -> 5-frame analyser features + FFN on split-f16 MFMA (HIP
 kernel) -> F-5 uint8 labels; with N > 1 ranks each rank classifies its own
 clip (weak scaling, no data-path collective) and the per-window decisions are
 gathered to rank 0 over RCCL inside the step (BASELINE configs 3 and 4).
+Consecutive steps alternate over --streams HIP streams (default 2, each with
+its own workspace and label buffer): step k + 1's MFCC kernel starts on the
+CUs that step k's MFCC tail and FFN leave idle; every step still runs its
+whole clip through both kernels inside the timed region.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--ffn bl13|ref39]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--ffn bl13|ref39] [--streams S]
 
 Rank 0 prints ONE JSON line.  `value` = frames (MFCC frames) processed by all
 ranks / max-over-ranks wall time of the K timed steps.  `roofline` is for the
@@ -329,7 +333,13 @@ def main():
     # a GPU that was idle starts at low clocks and ramps for ~30 ms of load:
     # warm-up steps continue (untimed) until this much warm-up time has passed
     ap.add_argument("--min-warmup-s", type=float, default=0.5)
+    # consecutive clips alternate over this many HIP streams (each with its
+    # own MFCC workspace and label buffer), so clip k + 1's MFCC fills the
+    # CUs that clip k's MFCC tail and FFN leave idle; 1 = strictly serial
+    ap.add_argument("--streams", type=int, default=2)
     args = ap.parse_args()
+    if args.streams < 1:
+        ap.error("--streams must be >= 1")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -365,10 +375,14 @@ def main():
     # gather completed (a stream-side wait, no host sync); every gather is
     # complete before the timed region ends.  gloo (the rehearsal on one GPU)
     # stages through the host and gathers synchronously.
-    labs = [labels, torch.empty_like(labels)] if world > 1 else [labels]
+    n_buf = max(args.streams, 2 if world > 1 else 1)
+    labs = [labels] + [torch.empty_like(labels) for _ in range(n_buf - 1)]
     gathers = [LabelGather(F - 5, dev) for _ in labs] if world > 1 else []
     pend = [None] * len(labs)
     k_step = [0]
+    # step k runs on streams[k % S] into label buffer k % n_buf; a buffer is
+    # always written from the same stream (n_buf is a multiple of S or S = 1)
+    streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
 
     def step():
         # vad_mfcc_ffn with a workspace: the MFCC kernel, then the window
@@ -376,12 +390,13 @@ def main():
         # forms on gfx950; the fused single kernel is timed below)
         i = k_step[0] % len(labs)
         k_step[0] += 1
-        if pend[i] is not None:
-            pend[i].wait()
-            pend[i] = None
-        pipe.labels(audio, out=labs[i])
-        if world > 1:
-            pend[i] = gathers[i].start(labs[i], async_op=args.backend == "nccl")
+        with torch.cuda.stream(streams[i % len(streams)]):
+            if pend[i] is not None:
+                pend[i].wait()
+                pend[i] = None
+            pipe.labels(audio, out=labs[i])
+            if world > 1:
+                pend[i] = gathers[i].start(labs[i], async_op=args.backend == "nccl")
 
     def drain():
         for i, w in enumerate(pend):
@@ -515,6 +530,7 @@ def main():
                                    "(25 ms frames, 10 ms hop, 512-pt FFT, 26 mel, 13 MFCC, "
                                    "analyser 5-frame features), labels gathered to rank 0",
                        "frames_per_gpu": F, "ffn": "-".join(map(str, topo)),
+                       "hip_streams": args.streams,
                        "parallelism": f"clip-shard x{world}"},
             "roofline": {"bound": "hbm", "kernel": dom,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

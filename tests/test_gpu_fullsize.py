@@ -136,6 +136,30 @@ def test_c3_full_clip_vs_oracle(torch_cuda):
     assert np.isnan(x).any(axis=1).sum() > 0  # digital silence exercised
 
 
+@pytest.mark.parametrize("n_streams", [2, 3])
+def test_c3_steps_alternating_streams(torch_cuda, n_streams):
+    """bench.py's pipelined step: consecutive 1M-frame clips alternate over
+    HIP streams (a workspace and a label buffer per stream, issued under
+    torch.cuda.stream), so one clip's MFCC overlaps the previous clip's
+    FFN; every buffer ends with the labels of the serial form, bit for bit."""
+    torch = torch_cuda
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 1_000_000
+    clips = [torch.from_numpy(O.synth_clip(O.samples_for_frames(F), seed=s)).cuda() for s in (1, 2)]
+    pipe = VadPipeline(FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)))
+    want = [pipe.labels(c).clone() for c in clips]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(n_streams - 1)]
+    labs = [torch.empty_like(want[0]) for _ in streams]
+    for k in range(4 * n_streams + 1):  # clips alternate too: a buffer's last clip is k % 2
+        with torch.cuda.stream(streams[k % n_streams]):
+            pipe.labels(clips[k % 2], out=labs[k % n_streams])
+    torch.cuda.synchronize()
+    last = {k % n_streams: k % 2 for k in range(4 * n_streams + 1)}
+    for i, lab in enumerate(labs):
+        assert torch.equal(lab, want[last[i]]), i
+
+
 @pytest.mark.parametrize("kernel", ["hop", "three"])
 def test_c5_512_streams_graph_replay(torch_cuda, golden, kernel):
     """C5: 512 concurrent streams, 40 hops of 10 ms each as hipGraph replays
