@@ -28,12 +28,22 @@ __device__ __forceinline__ Feat3 feature_triple(float a0, float a1, float a2, fl
                                                 int mode) {
   float mn = a2;
   if (mode == VAD_FEAT_ANALYSER) {
-    const float mean = ((((a0 + a1) + a2) + a3) + a4) * 0.2f;
-    const float e0 = a0 - mean, e1 = a1 - mean, e2 = a2 - mean, e3 = a3 - mean, e4 = a4 - mean;
-    const float var = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * 0.2f;
+    // e_i = a_i - sum / 5 as one fma each, written out: the rounding every
+    // kernel has used (clang contracted a_i - sum * 0.2f), now independent of
+    // how a kernel's code is vectorised or scheduled
+    const float sum = (((a0 + a1) + a2) + a3) + a4;
+    const float e0 = fmaf(sum, -0.2f, a0), e1 = fmaf(sum, -0.2f, a1), e2 = fmaf(sum, -0.2f, a2),
+                e3 = fmaf(sum, -0.2f, a3), e4 = fmaf(sum, -0.2f, a4);
+    // var * 2^24: v_rsq_f32 on a normal input for every var >= 2^-150,
+    // without the denormal-input fix-up rsqrtf wraps around it (five VALU
+    // operations per item); the 2^12 goes back into e2 exactly.  For every
+    // normal var the result is rsqrtf's bit for bit (v_rsq_f32(x 2^24) 2^12
+    // == v_rsq_f32(x) over all 1.93e9 normal x below 2^104 on gfx950,
+    // tools/checks/rsq_scale_check.hip)
+    const float var_s = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * (0.2f * 0x1p24f);
     const bool flat = (a0 == a1) & (a1 == a2) & (a2 == a3) & (a3 == a4);
     // branch-free: the NaN is added in rather than selected around the rsqrt
-    mn = e2 * rsqrtf(var) + (flat ? __builtin_nanf("") : 0.f);
+    mn = fmaf(e2 * 0x1p12f, __builtin_amdgcn_rsqf(var_s), flat ? __builtin_nanf("") : 0.f);
   }
   return {mn, a3 - a1, (a4 - mn) - (mn - a0)};
 }

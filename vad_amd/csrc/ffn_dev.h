@@ -535,6 +535,14 @@ struct LdsSlots {
 // ---------------------------------------------------------------------------
 constexpr int kWTile = 16;  // windows per wave tile
 
+// Lanes of one wave hand data to each other through LDS (rows -> features ->
+// operands).  A wave's LDS operations execute in order, so no wait is needed,
+// but in the language model each lane's accesses are independent and the
+// compiler may move one lane's store past a load of another address once no
+// branch separates them: this compiler barrier (no instruction) keeps the
+// hand-off order.
+__device__ __forceinline__ void wave_lds_handoff() { asm volatile("" ::: "memory"); }
+
 // Features (sklearn_analyser.py:52-69 / file_processing.py:51-66): item
 // i = 13 w + c is coefficient c of window w; its rows are R[i + 13 d].  A
 // flat coefficient (the analyser's 0/0: mn and d2 NaN) writes its features
@@ -545,6 +553,7 @@ template <int IN, int XS, int MODE>
 __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, float* __restrict__ X,
                                                    int* __restrict__ FL, int lane) {
   constexpr int MN = 13;
+  wave_lds_handoff();  // the rows R were stored by other lanes of this wave
   if (lane < kWTile) FL[lane] = 0;
 #pragma unroll
   for (int r = 0; r < (kWTile * MN + 63) / 64; ++r) {
@@ -563,6 +572,7 @@ __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, 
       }
     }
   }
+  wave_lds_handoff();  // other lanes read X / FL next (wave_tile_operands)
 }
 
 // Layer-0 B operands of window lane & 15 from X (lane (g, jw) holds

@@ -477,6 +477,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   // one tile: rows (prefetched two tiles ahead in `pre`) -> R; pre reloaded
   // with tile tn's rows; features -> X; MLP; label
   auto tile_body = [&](int64_t t, int64_t tn, float (&pre)[kWRowRegs]) {
+    wave_lds_handoff();  // the previous tile's reads of R / X / FL come first
 #pragma unroll
     for (int q = 0; q < kWRowRegs; ++q)
       if (lane + 64 * q < kWRows) R[lane + 64 * q] = pre[q];
