@@ -330,9 +330,11 @@ __device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1
 
 // out[mt] = bias + sum_s lo*hi + hi*lo + hi*hi (small terms first) on inputs
 // v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
-template <int TO, int KS, class FB, bool NONNEG = false, bool MERGE0 = false, class FH>
+// BOUNDED: the caller guarantees every input is finite and < 65504 in
+// magnitude, or an infinity (layer_scale's answer is 1 then too): no check.
+template <int TO, int KS, class FB, bool NONNEG = false, bool MERGE0 = false, bool BOUNDED = false, class FH>
 __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu) {
-  const float sc = layer_scale<KS, NONNEG>(v);
+  const float sc = BOUNDED ? 1.f : layer_scale<KS, NONNEG>(v);
   h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
@@ -457,12 +459,12 @@ struct FragLds {
 // Forward of one 16-window tile: x0 holds the layer-0 inputs of K-step s,
 // k = 8g + q (g = lane >> 4).
 template <int KS0, int T1, int T2, int T3, int T4, int NC, class FB, class FV, bool NOVL = false,
-          class FH>
+          bool IN_BOUNDED = false, class FH>
 __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)[(4 * KS0 + 31) / 32][8]) {
   using TP = Topo<KS0, T1, T2, T3, T4, NC, NOVL>;
   using HP = HTopo<TP, KS0, T1, T2, T3, T4>;
   f32x4 h1[T1];
-  dense_h3<T1, HP::K0, FB, false, kMerge0<KS0>>(fh, fb, x0, h1, TP::NL > 1);
+  dense_h3<T1, HP::K0, FB, false, kMerge0<KS0>, IN_BOUNDED>(fh, fb, x0, h1, TP::NL > 1);
   if constexpr (TP::NL == 1) return h1[0];
   else if constexpr (TP::NL == 2 && TP::VL) return valu_out_layer<TP, T1, FV>(fv, h1);
   else {
@@ -617,25 +619,35 @@ __device__ __forceinline__ int wave_tile_operands(const float* __restrict__ X, c
   return FL[jw];
 }
 
+// Analyser-mode inputs of a 13-input network are Mn = e2 / std alone: |Mn| <=
+// sqrt(5) whenever finite (e2^2 <= sum of the five e_i^2 = 5 var), a NaN
+// (flat or overflowed window: zeroed and flagged by the features) or +-inf
+// (var = 0 from underflowed squares) -- never a finite value past f16's
+// range, so layer 0 skips its range check (identical results).
+template <int MODE, int IN>
+constexpr bool wave_tile_in_bounded = MODE == VAD_FEAT_ANALYSER && IN == 13;
+
 // Label of window lane & 15 (valid on every lane) from its layer-0 operands:
 // the split-f16 forward, the NaN flag, argmax; z = its logits.
-template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, class FH, class FB, class FV>
+template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, bool IN_BOUNDED, class FH, class FB,
+          class FV>
 __device__ __forceinline__ int wave_tile_mlp(float (&x0)[(4 * KS0 + 31) / 32][8], int wnan, FH fh, FB fb, FV fv,
                                              int n_classes, f32x4& z) {
   if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
-  else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, FB, FV, NOVL>(fh, fb, fv, x0);
+  else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, FB, FV, NOVL, IN_BOUNDED>(fh, fb, fv, x0);
   if (wnan) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
   return argmax_classes(z, n_classes);
 }
 
-template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, int IN, int XS, bool MASK,
+// IN_BOUNDED (wave_tile_in_bounded): layer 0's inputs need no f16-range check
+template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, int IN, int XS, bool MASK, bool IN_BOUNDED,
           class FH, class FB, class FV>
 __device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, const int* __restrict__ FL,
                                                   int lane, FH fh, FB fb, FV fv, int n_classes, f32x4& z) {
   constexpr int K0 = (4 * KS0 + 31) / 32;
   float x0[K0][8];
   const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
-  return wave_tile_mlp<KS0, T1, T2, T3, T4, NC, NOVL>(x0, wnan, fh, fb, fv, n_classes, z);
+  return wave_tile_mlp<KS0, T1, T2, T3, T4, NC, NOVL, IN_BOUNDED>(x0, wnan, fh, fb, fv, n_classes, z);
 }
 
 // optional logits output (FfnDev::logits, tests): row w's fp32 logits

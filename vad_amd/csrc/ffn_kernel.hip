@@ -484,7 +484,8 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     load(tn < n_tiles ? tn : t, pre);
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
     f32x4 z;
-    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false>(
+    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
+                                       wave_tile_in_bounded<MODE, IN>>(
         X, FL, lane, fh, fbs, fvs, net.n_classes, z);
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) {

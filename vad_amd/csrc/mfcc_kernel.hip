@@ -1209,8 +1209,8 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     const LdsSlots fb{stbl + g4};
     const LdsSlots fv{stbl + 4 * TP::NB + g4};
     f32x4 z;
-    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true>(X, FL, lane, FragRegs{frh},
-                                                                                    fb, fv, net.n_classes, z);
+    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(
+        X, FL, lane, FragRegs{frh}, fb, fv, net.n_classes, z);
     const int64_t i = fs + (int64_t)tt * kTile - 4 + 16 * wave + (lane & 15);
     if (lane < 16 && i >= wb && i < we) labels[i] = (uint8_t)lab;
   };
