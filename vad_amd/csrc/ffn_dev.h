@@ -16,6 +16,10 @@ namespace vad {
 // argmax of softmax(z) with np.argmax semantics on the fp32 logits: any NaN
 // (or an all-NaN softmax from +inf / all -inf) -> class 0; else first max.
 __device__ __forceinline__ int argmax_classes(const f32x4 z, int n_classes) {
+  // two classes (n_classes is wave-uniform): the same rules in two compares --
+  // z1 > z0 is false when either is NaN, z0 = +inf or both are -inf, and
+  // z1 < +inf rejects z1 = +inf (and NaN); ties go to class 0 (first max)
+  if (n_classes == 2) return (z[1] > z[0]) & (z[1] < INFINITY);
   bool bad = false;
   float best = z[0];
   int arg = 0;
@@ -246,17 +250,32 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 
 constexpr float kH3Max = 65504.f;  // largest finite f16
 
+// v - f32(half SEL of the packed f16 pair hp), exact (v - f16(v) is a float):
+// one v_fma_mix_f32 (-hi * 1 + v, the f16 operand widened inside the fma)
+// instead of a conversion and a subtraction.  Inline asm is safe here: its
+// result goes to the v_cvt_pk_f16_f32 that forms the lo halves (a VALU read,
+// interlocked), never straight to an MFMA operand, whose read hazard after an
+// asm VALU write the compiler could not pad.
+template <int SEL>
+__device__ __forceinline__ float sub_f16_half(float v, unsigned hp) {
+  float d;
+  if constexpr (SEL == 0)
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hp), "v"(v));
+  else
+    asm("v_fma_mix_f32 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hp), "v"(v));
+  return d;
+}
+
 __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
-  // plain conversions, not v_fma_mix* inline asm (one instruction less per
-  // value, but the compiler cannot see an asm VALU write that a following
-  // MFMA reads as an operand, so it could not pad that hazard)
   u4 hw, lw;
 #pragma unroll
   for (int q = 0; q < 8; q += 2) {
     const f2 p = {v[q], v[q + 1]};
     const h2 h = __builtin_convertvector(p, h2);
-    const h2 r = __builtin_convertvector(p - __builtin_convertvector(h, f2), h2);
-    hw[q / 2] = __builtin_bit_cast(unsigned, h);
+    const unsigned hb = __builtin_bit_cast(unsigned, h);
+    const f2 d = {sub_f16_half<0>(v[q], hb), sub_f16_half<1>(v[q + 1], hb)};
+    const h2 r = __builtin_convertvector(d, h2);
+    hw[q / 2] = hb;
     lw[q / 2] = __builtin_bit_cast(unsigned, r);
   }
   hi = __builtin_bit_cast(h8, hw);
