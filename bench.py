@@ -410,17 +410,23 @@ def main():
     drain()
     torch.cuda.synchronize()
     extra = 0
-    while time.perf_counter() - t_w < args.min_warmup_s:
+    # every step issues a gather (N > 1), a collective: all ranks must run
+    # the same number of warm-up steps, so the time-based continuation is
+    # agreed on before each batch (any rank still short of the minimum warm-up
+    # keeps every rank going) -- a rank-local decision would leave the ranks'
+    # collectives mismatched
+    flag_dev = dev if args.backend == "nccl" else torch.device("cpu")
+    while True:
+        more = time.perf_counter() - t_w < args.min_warmup_s
+        if world > 1:
+            t = torch.tensor([int(more)], dtype=torch.int64, device=flag_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            more = bool(t.item())
+        if not more:
+            break
         for _ in range(10):
             step()
         extra += 10
-        drain()
-        torch.cuda.synchronize()
-    if world > 1:  # every rank warms up equally long
-        t = torch.tensor([extra], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        for _ in range(int(t.item()) - extra):
-            step()
         drain()
         torch.cuda.synchronize()
     if world > 1:
@@ -435,7 +441,7 @@ def main():
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=flag_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     # per-kernel launch durations, right after the timed region: HIP events
@@ -471,7 +477,7 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         tg = time.perf_counter() - tg
-        t = torch.tensor([tg], dtype=torch.float64, device=dev)
+        t = torch.tensor([tg], dtype=torch.float64, device=flag_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         gather = {"gather_ms": float(t.item()) * 1e3 / n_g, "label_bytes_per_rank": F - 5,
                   "collective": "gather" if gathers[0].use_gather else "all_gather",
