@@ -355,7 +355,7 @@ def main():
 
     from vad_amd.ffn import TOPOLOGY_BL13, TOPOLOGY_REF39, FFNClassifier, random_layers
     from vad_amd.pipeline import VadPipeline
-    from vad_amd.dist import LabelGather
+    from vad_amd.dist import LabelGather, any_rank
 
     topo = TOPOLOGY_BL13 if args.ffn == "bl13" else TOPOLOGY_REF39
     layers = random_layers(topo, seed=3)
@@ -416,14 +416,7 @@ def main():
     # keeps every rank going) -- a rank-local decision would leave the ranks'
     # collectives mismatched
     flag_dev = dev if args.backend == "nccl" else torch.device("cpu")
-    while True:
-        more = time.perf_counter() - t_w < args.min_warmup_s
-        if world > 1:
-            t = torch.tensor([int(more)], dtype=torch.int64, device=flag_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            more = bool(t.item())
-        if not more:
-            break
+    while any_rank(time.perf_counter() - t_w < args.min_warmup_s, flag_dev):
         for _ in range(10):
             step()
         extra += 10

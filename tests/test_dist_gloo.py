@@ -133,3 +133,39 @@ def test_sharded_clip_labels_equal_whole_clip(world):
         p.join(timeout=120)
         assert p.exitcode == 0
     assert same
+
+
+def _warmup_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from vad_amd.dist import LabelGather, any_rank
+    g = LabelGather(4, torch.device("cpu"))
+    # bench.py's warm-up shape: every trip holds a collective (the step's
+    # gather) and the continuation is rank-local (here: rank r wants 2 + 2r
+    # trips); any_rank makes every rank run the longest rank's trips
+    trips = 0
+    while any_rank(trips < 2 + 2 * rank):
+        g(torch.full((4,), rank, dtype=torch.uint8))
+        trips += 1
+    q.put((rank, trips))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_warmup_continuation_agreed_across_ranks(world):
+    """Regression (the 2-rank bench rehearsal hung when the ranks' time-based
+    warm-up ran different numbers of gathering steps): with any_rank every
+    rank runs the same number of trips, so the collectives stay matched."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_warmup_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == {r: 2 + 2 * (world - 1) for r in range(world)}

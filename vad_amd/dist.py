@@ -112,6 +112,20 @@ def gather_labels(labels: torch.Tensor, dst=0, group=None):
     return [o[:s] for o, s in zip(out, sizes)] if rank == dst else None
 
 
+def any_rank(flag: bool, device=None, group=None) -> bool:
+    """True on every rank when `flag` is True on any rank (an all_reduce MAX;
+    `device` the backend's: a CUDA device with nccl, the CPU with gloo).  For
+    loops whose body holds a collective and whose continuation is decided per
+    rank (bench.py's time-based warm-up): agreeing before each trip keeps the
+    ranks' collectives matched -- a rank-local decision can leave one rank in
+    the loop's collective while another has moved on to the next one."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return bool(flag)
+    t = torch.tensor([int(bool(flag))], dtype=torch.int64, device=device or torch.device("cpu"))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(t.item())
+
+
 class LabelGather:
     """Gather of a fixed-size uint8 label tensor from every rank to `dst`,
     with the receive buffers allocated once: one collective per call, no
