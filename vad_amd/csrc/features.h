@@ -15,11 +15,11 @@ namespace vad {
 // of five floats fits a double), so x - mean = 0 and Mn = 0/0 = NaN, exactly
 // as numpy gives on these MFCCs; fp32 rounding of the mean could instead
 // leave a tiny non-zero std and a finite Mn, so flatness is tested
-// explicitly.  (The reference's MFCCs are fp64: on a digital-silence window
-// its fp64 5-sum rounds at some coefficients -- c4 and c7 of the 26-filter
-// silence MFCC -- and it gets Mn = +-1 there instead of NaN.  FFN labels are
-// unaffected -- any NaN feature makes the window class 0 in both -- but a
-// decision tree sees NaN where the reference sees +-1: DESIGN.md section 2.)
+// explicitly.  The reference run agrees: in tests/golden/analyser.npz every
+// digital-silence window has all 13 Mn (and D2) NaN in the row the reference
+// passed to predict, the positions the kernels give (DESIGN.md section 2;
+// only the oracle's explicit fp64 DCT matrix rounds a silent coefficient
+// differently from frame to frame).
 struct Feat3 {
   float mn, d1, d2;
 };
