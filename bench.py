@@ -270,31 +270,46 @@ def secondary_configs(dev, reps=60):
             "note": "6 rotated 64 MB clips (384 MB working set)"}
     del clips
     S = 512
-    # BASELINE configs[4]: 512 streams, hipGraph-captured hops.  Per hop of
-    # every stream: the one-kernel hop launched directly (input read in
-    # place); captured one hop per replay (the graph reads its static input
-    # block in place: a producer writes the next hop there) and, as round 2
-    # timed it, with an eager copy into that block before each replay; K = 8
-    # hops per launch (vad_stream_hops: tables staged once per launch, stream
-    # state carried in registers), direct and captured (the form a replay per
-    # 80 ms of audio takes); the three-kernel form captured.
+    # BASELINE configs[4]: 512 streams, hipGraph-captured hops.  Device-input
+    # lines (the hop block already in HBM): the one-kernel hop launched
+    # directly (input read in place); captured one hop per replay with an
+    # eager copy into its static block before each replay (the round-2 form
+    # of this key); captured reading the static block in place; K = 8 hops
+    # per launch (vad_stream_hops: tables staged once per launch, stream
+    # state carried in registers), direct and captured; the three-kernel form
+    # captured.  End-to-end lines (C5's rate includes the H2D
+    # copy): each step copies the 512 x 160 new samples of its K hops from
+    # pinned host memory, runs the hop kernel and copies the K x 512 labels
+    # back (StreamBatch.step_host), launched directly or as ONE graph replay
+    # (vad_graph_launch) -- us_per_hop back to back, and latency_us = one
+    # step until its labels are in host memory (stream sync, host clock).
     clf = FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3))
-    for name, kernel, K, graph, copy in (("hop_kernel", "hop", 1, False, False),
-                                         ("hop_kernel_hipgraph", "hop", 8, True, False),
-                                         ("hop_kernel_x8", "hop", 8, False, False),
-                                         ("hop_kernel_hipgraph_1hop", "hop", 1, True, False),
-                                         ("hop_kernel_hipgraph_1hop_with_copy", "hop", 1, True, True),
-                                         ("three_kernel_hipgraph", "three", 1, True, True)):
+    for name, kernel, K, graph, copy, host in (
+            ("hop_kernel", "hop", 1, False, False, False),
+            ("hop_kernel_hipgraph", "hop", 1, True, True, False),
+            ("hop_kernel_hipgraph_1hop", "hop", 1, True, False, False),
+            ("hop_kernel_x8", "hop", 8, False, False, False),
+            ("hop_kernel_hipgraph_x8", "hop", 8, True, False, False),
+            ("three_kernel_hipgraph", "three", 1, True, True, False),
+            ("e2e_host_io_direct", "hop", 1, False, False, True),
+            ("e2e_host_io_hipgraph", "hop", 1, True, False, True),
+            ("e2e_host_io_direct_x8", "hop", 8, False, False, True),
+            ("e2e_host_io_hipgraph_x8", "hop", 8, True, False, True)):
         sb = StreamBatch(S, clf, kernel=kernel, hops_per_step=K)
         g = torch.Generator(device=dev).manual_seed(500)
         sb.prime(torch.randn((S, 240), generator=g, device=dev) * 1000)
         blocks = [torch.randn((K, S, 160), generator=g, device=dev) * 1000 for _ in range(8)]
         sb.inputs.copy_(blocks[0])
+        if host:
+            sb.attach_host_io()
+            sb.host_inputs.copy_(blocks[0].cpu())
         if graph:
-            sb.capture()
+            sb.capture(host_io=host)
 
         def one(k):
-            if graph and not copy:
+            if host:
+                sb.step_host()  # the producer writes host_inputs between steps
+            elif graph and not copy:
                 sb.step_block()  # the static block, written in place by the producer
             elif K == 1:
                 sb.step(blocks[k % 8][0])
@@ -312,10 +327,38 @@ def secondary_configs(dev, reps=60):
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / (reps * K) * 1e3
-        out[f"c5_512_streams_{name}"] = {"us_per_hop": us, "stream_frames_per_s": S / (us * 1e-6),
-                                         "x_real_time": 10_000.0 / us, "hops_per_launch_or_replay": K,
-                                         "hipgraph": graph, "input_copy_per_step": copy}
+        rec = {"us_per_hop": us, "stream_frames_per_s": S / (us * 1e-6),
+               "x_real_time": 10_000.0 / us, "hops_per_launch_or_replay": K,
+               "hipgraph": graph, "input_copy_per_step": copy or host,
+               "host_io": host}
+        if host:
+            cur = torch.cuda.current_stream()
+            lat = []
+            for k in range(200):
+                t0 = time.perf_counter()
+                one(k)
+                cur.synchronize()
+                lat.append(time.perf_counter() - t0)
+            lat = np.sort(np.asarray(lat)) * 1e6
+            rec["bytes_per_step"] = {"h2d": K * S * 160 * 4, "d2h": K * S}
+            rec["latency_us"] = {"p50": float(lat[len(lat) // 2]), "p90": float(lat[int(0.9 * len(lat))]),
+                                 "mean": float(lat.mean())}
+        out[f"c5_512_streams_{name}"] = rec
     return out
+
+
+def launch_ranks(n):
+    """Run this script as n ranks under torch.distributed.run (127.0.0.1, a
+    free port); called before any GPU call of the parent process, which only
+    waits for the children (no exec)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -340,8 +383,20 @@ def main():
     args = ap.parse_args()
     if args.streams < 1:
         ap.error("--streams must be >= 1")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # --gpus N without a launcher: start N rank processes (one per GPU)
+        # under torch.distributed.run before this process touches the GPU,
+        # and exit with their status (rank 0 prints the JSON line)
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={env_world}", file=sys.stderr)
+        sys.exit(2)
+
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     local = local % torch.cuda.device_count() if args.backend == "gloo" else local
@@ -383,6 +438,8 @@ def main():
     # step k runs on streams[k % S] into label buffer k % n_buf; a buffer is
     # always written from the same stream (n_buf is a multiple of S or S = 1)
     streams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(args.streams - 1)]
+    for s in streams[1:]:
+        s.wait_stream(stream)  # synth_audio wrote the clip on the default stream
 
     def step():
         # vad_mfcc_ffn with a workspace: the MFCC kernel, then the window
@@ -437,6 +494,22 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device=flag_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    # the same K steps strictly serial on one stream (no gathers): the latency
+    # of one clip through both kernels, beside the pipelined headline
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for k in range(args.steps):
+        pipe.labels(audio, out=labels)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ts = time.perf_counter() - ts
+    if world > 1:
+        t = torch.tensor([ts], dtype=torch.float64, device=flag_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ts = float(t.item())
     # per-kernel launch durations, right after the timed region: HIP events
     # around `steps` back-to-back launches of one kernel (an event record
     # between two kernels idles the GPU for ~5 us, so the timed steps carry
@@ -514,6 +587,11 @@ def main():
             "warmup": args.warmup,
             "warmup_extra_steps": extra,
             "ms_per_step": el * 1e3 / args.steps,
+            "ms_per_step_note": (f"pipelined throughput: consecutive steps alternate over {args.streams} HIP "
+                                 "streams, so a step's MFCC overlaps the previous step's FFN; "
+                                 "ms_per_step_serial is the same K steps on one stream")
+            if args.streams > 1 else "steps serial on one stream",
+            "ms_per_step_serial": ts * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

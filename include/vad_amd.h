@@ -296,7 +296,9 @@ int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* fr
  * plan tables are staged into LDS once per launch instead of once per hop;
  * the form a hipGraph captures for many hops per replay (n_hops = 1 is
  * vad_stream_hop).  Same refusals as vad_stream_hop, plus VAD_EINVAL for
- * n_hops < 0 or (n_hops > 1 and label_block_stride < n_streams). */
+ * n_hops < 0, or n_hops > 1 with label_block_stride < n_streams or
+ * hop_block_stride < (n_streams - 1) * hop_stride + hop_len (hop blocks that
+ * overlap, repeat or run backwards). */
 int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
                     int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
                     int32_t n_hops, int64_t hop_block_stride, float* ring, int32_t* count, uint8_t* labels,
@@ -304,6 +306,13 @@ int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* f
 int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const float* frames,
                     int64_t frame_stride, int32_t frame_len, int64_t n_streams, float* ring,
                     int32_t* count, uint8_t* labels, float* mfcc_scratch, void* stream);
+/* Replay a captured hipGraph (hipGraphExec_t) on `stream`: the per-hop step
+ * of a StreamBatch captured with its host I/O (the H2D copy of every
+ * stream's new samples from pinned memory, the hop kernel, the D2H copy of
+ * the labels -- vad.py:32-59's loop body for S streams).  The capture itself
+ * is the host's (hipStreamBeginCapture / torch.cuda.graph); this entry only
+ * launches, so a host replays without a runtime wrapper in between. */
+int vad_graph_launch(void* graph_exec, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU clip sharding: one process per GPU, each

@@ -10,6 +10,8 @@ the driver's 8-GPU run.
 import os
 import socket
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 import pytest
 import torch.multiprocessing as mp
 
@@ -171,3 +173,25 @@ def test_capi_rccl_world1_gather():
     p.join(timeout=60)
     assert status == "ok" and ok is True, ok
     assert p.exitcode == 0
+
+
+def test_bench_gpus_launches_ranks():
+    """`bench.py --gpus 2` with no launcher starts the two rank processes
+    itself (torch.distributed.run on 127.0.0.1): rank 0 prints one JSON line
+    with n_gpus 2 and the gather object (gloo: both ranks share the one GPU
+    of the test box)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--frames", "20000", "--steps", "2", "--warmup", "1", "--no-cpu", "--no-secondary",
+                        "--min-warmup-s", "0.05"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "clip-shard x2"
+    assert out["gather"]["label_bytes_per_rank"] == 20000 - 5 and out["gather"]["backend"] == "gloo"
+    assert out["value"] > 0

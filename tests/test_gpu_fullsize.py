@@ -16,12 +16,16 @@ import numpy as np
 import pytest
 
 from oracle import vad_oracle as O
+from label_report import label_agreement
 
 pytestmark = pytest.mark.gpu
 
 MFCC_TOL = 1e-4
 LABEL_MARGIN = 0.05
 SPLIT_VS_F32 = 2.5  # measured 1.05x (13-64-64-2) and 1.5x (39-64-32-16-3)
+# windows of the C3 clip whose label differs from the fp64 oracle (all of them
+# below LABEL_MARGIN; the count and margins are reported by label_agreement)
+C3_MAX_DISAGREE = 20
 
 
 @pytest.fixture(scope="module")
@@ -124,9 +128,11 @@ def test_c3_full_clip_vs_oracle(torch_cuda):
     marg = O.ffn_margin(x, layers)
     assert got.shape == ref_l.shape == (F - 5,)
     sure = marg > LABEL_MARGIN
+    rep = label_agreement(got, ref_l, marg, name="label_agreement_c3",
+                          extra={"config": "C3 1M frames, 13-64-64-2 seed 3, clip seed 1",
+                                 "below_label_margin": int((~sure).sum()), "label_margin": LABEL_MARGIN})
     np.testing.assert_array_equal(got[sure], ref_l[sure])
-    bad = int((got != ref_l).sum())
-    assert bad <= 20, (bad, int((~sure).sum()))
+    assert rep["disagree"] <= C3_MAX_DISAGREE, rep["disagree_windows"]
     # and exactly the oracle's FFN on the device's own features where the
     # margin clears the forward's rounding
     xg = window_features(m).cpu().numpy()[:, :13]

@@ -511,6 +511,63 @@ def test_stream_hop_blocks_equal_single_hops(torch_cuda, golden, kernel, K):
     assert (want[:5] == 255).all() and (want[5:] != 255).all()
 
 
+@pytest.mark.parametrize("K,graph", [(1, False), (1, True), (8, False), (8, True)])
+def test_stream_host_io_steps(torch_cuda, golden, K, graph):
+    """C5 as SURVEY 8(d) times it: each step copies every stream's new
+    samples from pinned host memory, runs the hop kernel and copies the
+    labels back (step_host; captured into the hipGraph with host_io=True and
+    replayed through vad_graph_launch): the host labels equal the
+    device-input single-hop steps', and the state ends identical."""
+    import torch
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    S, nb = 512, 4
+    T = K * nb
+    clips = np.stack([O.synth_clip(160 * (T - 1) + 401, seed=900 + s) for s in range(S)])
+    carry = torch.from_numpy(np.ascontiguousarray(clips[:, :240])).cuda()
+    hops = np.ascontiguousarray(np.stack([clips[:, 240 + 160 * t: 400 + 160 * t] for t in range(T)]))
+    ref = StreamBatch(S, clf)
+    ref.prime(carry)
+    want = torch.stack([ref.step(torch.from_numpy(hops[t]).cuda()).clone() for t in range(T)]).cpu()
+    sb = StreamBatch(S, clf, hops_per_step=K)
+    sb.prime(carry)
+    if graph:
+        sb.capture(host_io=True)
+    else:
+        sb.attach_host_io()
+    got = []
+    for b in range(nb):
+        sb.host_inputs.copy_(torch.from_numpy(hops[b * K:(b + 1) * K]))
+        lab = sb.step_host()
+        torch.cuda.current_stream().synchronize()
+        got.append(lab.clone())
+    got = torch.cat(got)
+    assert torch.equal(got, want), int((got != want).sum())
+    assert torch.equal(sb.frames, ref.frames) and torch.equal(sb.ring, ref.ring)
+    assert (want[5:] != 255).all()
+
+
+def test_stream_hops_rejects_overlapping_blocks(torch_cuda, golden):
+    """vad_stream_hops refuses hop blocks that repeat or overlap (a zero or
+    short hop_block_stride with n_hops > 1) before launching anything."""
+    import ctypes
+    import torch
+    from vad_amd import _lib
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    sb = StreamBatch(4, FFNClassifier(layers_from(w, "ref39", 4)), hops_per_step=2)
+    L = _lib.lib()
+    for bs in (0, -640, 3 * 160):
+        rc = L.vad_stream_hops(sb.plan.handle, sb.ffn.plan.handle, _lib.ptr(sb.frames), 400, 400,
+                               _lib.ptr(sb.inputs), 160, 160, 4, 2, bs, _lib.ptr(sb.ring), _lib.ptr(sb.count),
+                               _lib.ptr(sb.label_block), 4, _lib.stream_ptr())
+        assert rc == _lib.VAD_EINVAL, (bs, rc)
+    assert (sb.count == 0).all()  # nothing ran
+
+
 @pytest.mark.parametrize("frame_size,hop,nf", [(512, 256, 26), (1000, 400, 26), (400, 160, 40)])
 def test_stream_hop_long_frames(torch_cuda, golden, frame_size, hop, nf):
     """Frames longer than 448 samples take the hop kernel's 16-chunk build

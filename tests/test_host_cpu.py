@@ -195,3 +195,16 @@ def test_sharded_clip_rejects_segment_preemphasis():
     seg = torch.zeros((sh.sample_hi - sh.sample_lo,))
     with pytest.raises(ValueError):
         classify_clip_shard(_Pipe(), seg, sh)
+
+
+def test_bench_refuses_world_size_mismatch():
+    """bench.py exits non-zero, before any GPU call, when a launcher's
+    WORLD_SIZE disagrees with --gpus (a silent N = 1 run is not a scaling
+    point)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "1", "--no-cpu"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "disagrees with WORLD_SIZE" in r.stderr

@@ -74,6 +74,7 @@ SIGNATURES = {
                                 c_vp, c_vp, c_i64, c_vp]),
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                 c_vp]),
+    "vad_graph_launch": (c_int, [c_vp, c_vp]),
     "vad_rccl_available": (c_int, []),
     "vad_rccl_error_string": (ctypes.c_char_p, []),
     "vad_rccl_unique_id": (c_int, [c_vp]),

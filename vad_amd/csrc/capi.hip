@@ -830,6 +830,9 @@ int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* f
       hop_len > frame_len || frame_stride < frame_len || hop_stride < hop_len)
     return VAD_EINVAL;
   if (n_hops > 1 && label_block_stride < n_streams) return VAD_EINVAL;  // label rows of two hops would overlap
+  // hop k's block must not be hop k-1's: a zero or negative stride would
+  // replay (or walk backwards over) the new samples
+  if (n_hops > 1 && hop_block_stride < (n_streams - 1) * hop_stride + hop_len) return VAD_EINVAL;
   if (n_streams == 0 || n_hops == 0) return VAD_OK;
   if (!frames || !hop || !ring || !count || !labels) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;
@@ -863,6 +866,13 @@ int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const fl
     VAD_TRY(launch_mfcc(0, plan->dev, launch_spec(plan), frames, frame_stride, frame_len, n_streams, mfcc_scratch, st));
   return (int)launch_stream_ffn(ffn->net, mfcc_scratch, ring, count, n_streams, plan->host.mfcc_n,
                                 labels, st);
+}
+
+// Replay of a captured graph (a hop block with its host copies,
+// vad_amd.stream.StreamBatch.capture): hipGraphLaunch on the caller's stream.
+int vad_graph_launch(void* graph_exec, void* stream) {
+  if (!graph_exec) return VAD_EINVAL;
+  return (int)hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -462,30 +462,8 @@ __device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
                                               float* __restrict__ lm);
 template <class T, int G>
 __device__ __forceinline__ void dct_code(const float* __restrict__ lm, float (&acc)[4]);
-template <class T, int W>
-__device__ __forceinline__ void mel_band12_code(const float* __restrict__ prow, float* __restrict__ lm);
 
 #include "mel_code.h"
-
-// the 12-band split of mfcc3_kernel's phase 2a (wave w: band w)
-template <class T>
-__device__ __forceinline__ void mel12_dispatch(int wave, const float* prow, float* lrow) {
-  prow = static_cast<const float*>(__builtin_assume_aligned(prow, 16));
-  switch (wave) {
-    case 0: mel_band12_code<T, 0>(prow, lrow); break;
-    case 1: mel_band12_code<T, 1>(prow, lrow); break;
-    case 2: mel_band12_code<T, 2>(prow, lrow); break;
-    case 3: mel_band12_code<T, 3>(prow, lrow); break;
-    case 4: mel_band12_code<T, 4>(prow, lrow); break;
-    case 5: mel_band12_code<T, 5>(prow, lrow); break;
-    case 6: mel_band12_code<T, 6>(prow, lrow); break;
-    case 7: mel_band12_code<T, 7>(prow, lrow); break;
-    case 8: mel_band12_code<T, 8>(prow, lrow); break;
-    case 9: mel_band12_code<T, 9>(prow, lrow); break;
-    case 10: mel_band12_code<T, 10>(prow, lrow); break;
-    default: mel_band12_code<T, 11>(prow, lrow); break;
-  }
-}
 
 template <class T>
 __device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float* lrow) {
@@ -1287,399 +1265,8 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
   }
 }
 
-// ---------------------------------------------------------------------------
-// mfcc3_kernel: the reference framing (400 / 160) at THREE waves per SIMD.
-//
-// The two-wave kernel above is VALU-issue bound: while one wave of a SIMD
-// waits (barrier, LDS, loads) its partner issues alone at half rate.  A
-// third wave needs <= 160 KB / 12 waves of LDS and <= 168 VGPRs; this
-// dataflow fits both:
-//   * one 768-thread workgroup (12 waves) per CU, 96-frame tiles: lane group
-//     g (16 lanes) runs frames 2g (pass 0) and 2g + 1 (pass 1) from one
-//     18-chunk sample buffer, as the paired-frame loop does;
-//   * no separate power tile: each group's 2304-B transpose block is also
-//     where its two frames' power rows go.  Pass 0's 16 power values wait in
-//     registers until pass 1's transpose reads are issued (LDS is in order
-//     per wave), then both rows are written into the block;
-//   * the per-lane FFT twiddles are read from a 3.5 KB LDS table where they
-//     are used (48 VGPRs fewer than keeping them resident);
-//   * phase 2a (frame per lane): waves 0..7 take the 8 filter bands of
-//     frames 0..63, waves 8..11 two bands each of frames 64..95 (32 lanes);
-//     phase 2b (lifter x DCT) of the previous tile runs before the first
-//     barrier on waves 0..3 (frames 0..63) and 4..7 (frames 64..95).
-// Power-row placement: frame 2g + p of group g starts at bank 4 (g mod 16)
-// (+ 32 for pass 1), so the frame-per-lane ds_read_b128 of phase 2a hits 16
-// distinct bank quads in every lane group; the transpose layout keeps the
-// block base at bank 0 as above.
-// ---------------------------------------------------------------------------
-constexpr int kW3 = 12;
-constexpr int kThreads3 = 64 * kW3;
-constexpr int kGroups3 = kThreads3 / 16;   // 48
-constexpr int kTile3 = 2 * kGroups3;       // 96 frames
-constexpr int kRegion3 = 2 * kGroupScratch;  // floats per group block (576 = 2304 B)
-constexpr int kLmRows3 = 128;              // frames 0..63, then 64..95 (+ 32 unused rows)
-
-template <int SPEC>
-constexpr size_t mfcc3_smem_bytes() {
-  return (size_t)kGroups3 * kRegion3 * sizeof(float) + (size_t)kLmRows3 * lm_stride<SPEC>() * sizeof(float) +
-         kTwLdsBytes + (size_t)4 * dct_k_steps<SPEC>() * 16 * sizeof(float);
-}
-
-// float offset of frame 2g + p's power row (bins 0..255) in the blocks
-__device__ __forceinline__ int row_off3(int g, int p) {
-  const int gp = g & 15;
-  int a, b;  // rows of pass 0 / pass 1 inside block g: 256 floats each, 32 apart
-  if (gp <= 8) {
-    a = 4 * gp;
-    b = a + 288;
-  } else {
-    b = 4 * gp - 32;
-    a = b + 288;
-  }
-  return g * kRegion3 + (p ? b : a);
-}
-
-// stage A with the per-lane twiddles W256^(j k1) read from the LDS table
-template <typename TIN, int NZ, int LEN, int OFF, int NB>
-__device__ __forceinline__ void stage_a_lds(const v2f (&buf)[NB], const v4f* __restrict__ twa4, int j,
-                                            v2f (&u)[16]) {
-#pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);  // chunk c in slot c mod NB
-  pad_stage_a<NZ, LEN, 16>(LEN, j, u);
-  pk::dft16<NZ>(u);
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const v4f t = twa4[q];
-    if (q > 0) u[2 * q] = pk::cmul(u[2 * q], t.xy);
-    u[2 * q + 1] = pk::cmul(u[2 * q + 1], t.zw);
-  }
-}
-
-// one 16-entry column of a transpose block (8 ds_read_b128)
-__device__ __forceinline__ void read_col(int c, const v2f* __restrict__ scr, v2f (&col)[16]) {
-  const v4f* cp = reinterpret_cast<const v4f*>(__builtin_assume_aligned(scr + c * kColStride, 16));
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const v4f t = cp[q];
-    col[2 * q] = t.xy;
-    col[2 * q + 1] = t.zw;
-  }
-}
-
-// the real-FFT split + power of finish_b on E (even half of column cE) and O
-// (odd half of column cO), twiddles W512^kE(m) from registers (TWB) or LDS
-template <bool TWREG>
-__device__ __forceinline__ void split_pw(const LaneConsts& L, const v4f* __restrict__ twb4, const v2f (&E)[8],
-                                         const v2f (&O)[8], float (&pkv)[8], float (&pnv)[8]) {
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    v2f tw;
-    if constexpr (TWREG) {
-      tw = L.twb[m];
-    } else {
-      const v4f tq = twb4[m >> 1];
-      tw = (m & 1) ? tq.zw : tq.xy;
-    }
-    const v2f a = (m >= 4 && L.col0) ? O[m] : E[m];
-    const v2f b = (m < 4 && L.col0) ? E[m == 0 ? 4 : (8 - m) & 7] : O[7 - m];
-    const v2f S = pk::add_conj(a, b);
-    const v2f T = pk::cmul(pk::sub_conj(a, b), tw);
-    const v2f U = pk::split_u(S, T);
-    const v2f V = pk::split_v(S, T);
-    const v2f p2 = U * U + V * V;
-    float pk = p2.x, pn = p2.y;
-    if (m == 0) {  // lane 14: bins 0 and 128 are their own partners
-      const float s0 = a.x + a.y;
-      pk = L.col0 ? 4.f * s0 * s0 : pk;
-      pn = L.col0 ? 4.f * fmaf(b.x, b.x, b.y * b.y) : pn;
-    }
-    pkv[m] = pk;
-    pnv[m] = pn;
-  }
-}
-
-// stage A with the per-lane twiddles in registers
-template <typename TIN, int NZ, int LEN, int OFF, int NB>
-__device__ __forceinline__ void stage_a_reg(const v2f (&buf)[NB], const LaneConsts& L, int j, v2f (&u)[16]) {
-#pragma unroll
-  for (int n = 0; n < NZ; ++n) u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);  // chunk c in slot c mod NB
-  pad_stage_a<NZ, LEN, 16>(LEN, j, u);
-  pk::dft16<NZ>(u);
-#pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) u[k1] = pk::cmul(u[k1], L.twa[k1]);
-}
-
-// finish_b's arithmetic with W512^kE(m) read from the LDS table; the 16
-// power values |2X|^2 (2^-20 folded into the taps) into registers
-__device__ __forceinline__ void finish_b_pw(const LaneConsts& L, const v4f* __restrict__ twb4, v2f (&col)[32],
-                                            float (&pkv)[8], float (&pnv)[8]) {
-  v2f E[8], O[8];
-  pk::dft16_even(*reinterpret_cast<v2f(*)[16]>(&col[0]), E);
-  pk::dft16_odd(*reinterpret_cast<v2f(*)[16]>(&col[16]), O);
-#pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    const v4f tq = twb4[m >> 1];
-    const v2f tw = (m & 1) ? tq.zw : tq.xy;
-    const v2f a = (m >= 4 && L.col0) ? O[m] : E[m];
-    const v2f b = (m < 4 && L.col0) ? E[m == 0 ? 4 : (8 - m) & 7] : O[7 - m];
-    const v2f S = pk::add_conj(a, b);
-    const v2f T = pk::cmul(pk::sub_conj(a, b), tw);
-    const v2f U = pk::split_u(S, T);
-    const v2f V = pk::split_v(S, T);
-    const v2f p2 = U * U + V * V;
-    float pk = p2.x, pn = p2.y;
-    if (m == 0) {  // lane 14: bins 0 and 128 are their own partners
-      const float s0 = a.x + a.y;
-      pk = L.col0 ? 4.f * s0 * s0 : pk;
-      pn = L.col0 ? 4.f * fmaf(b.x, b.x, b.y * b.y) : pn;
-    }
-    pkv[m] = pk;
-    pnv[m] = pn;
-  }
-}
-
-// the 16 stores of finish_b (paired into ds_write2_b32 by base)
-__device__ __forceinline__ void store_pw(const LaneConsts& L, const float (&pkv)[8], const float (&pnv)[8],
-                                         float* __restrict__ prow) {
-  float* pe0 = prow + L.e0;
-  float* pe4 = prow + L.e0 + L.off4;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) pe0[32 * m] = pkv[m];
-#pragma unroll
-  for (int m = 4; m < 8; ++m) pe4[32 * m] = pkv[m];
-  prow[L.kO0] = pnv[0];
-  float* po0 = prow + 256 - L.e0;
-#pragma unroll
-  for (int m = 1; m < 4; ++m) po0[-32 * m] = pnv[m];
-  float* po4 = prow + 256 - L.e0 - L.off4;
-#pragma unroll
-  for (int m = 4; m < 8; ++m) po4[-32 * m] = pnv[m];
-}
-
-#ifndef VAD_M3_PRIO
-#define VAD_M3_PRIO 1  // milestone priorities 3 -> 0 through phase 1 (lagging waves catch up)
-#endif
-#ifndef VAD_M3_TW
-#define VAD_M3_TW 0  // per-lane FFT twiddles: 0 both tables from LDS, 1 stage A's in VGPRs, 2 both in VGPRs
-#endif
-#ifndef VAD_M3_DIAG
-#define VAD_M3_DIAG 0  // diagnostic builds only (outputs wrong): 1 phase 1 alone, 2 phase 1 + barriers
-#endif
-#ifndef VAD_M3_BUF13
-#define VAD_M3_BUF13 0  // 1: 13 sample slots (pass 1's last 5 chunks loaded during the tile) instead of 18
-#endif
-#ifndef VAD_M3_SPLITREAD
-#define VAD_M3_SPLITREAD 0  // 1: column cE read and its even half computed before column cO is read
-#endif
-#define M3_STAMP(k)                                      \
-  do {                                                   \
-    if constexpr (VAD_M3_DIAG == 5) {                    \
-      __builtin_amdgcn_sched_barrier(0);                 \
-      st_[k] = __builtin_amdgcn_s_memtime();             \
-      __builtin_amdgcn_sched_barrier(0);                 \
-    }                                                    \
-  } while (0)
-#define M3_PRIO(k)                                       \
-  do {                                                   \
-    if constexpr (VAD_M3_PRIO != 0) {                    \
-      __builtin_amdgcn_sched_barrier(0);                 \
-      __builtin_amdgcn_s_setprio(k);                     \
-      __builtin_amdgcn_sched_barrier(0);                 \
-    }                                                    \
-  } while (0)
-
-template <typename TIN, int SPEC>
-__global__ __launch_bounds__(kThreads3, 1) void mfcc3_kernel(const MfccDev* __restrict__ plan,
-                                                             const TIN* __restrict__ src, int64_t n_frames,
-                                                             float* __restrict__ out) {
-  using T = std::conditional_t<SPEC == 1, Mel26, Mel40>;
-  constexpr int LEN = 400, NZ = 13, HOPC = 5, NC18 = NZ + HOPC, LMS = lm_stride<SPEC>();
-  constexpr int NB = VAD_M3_BUF13 ? NZ : NC18;  // sample slots (chunk c in slot c mod NB)
-  constexpr int MN = T::NC;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* R = reinterpret_cast<float*>(smem);                 // 48 group blocks
-  float* lm = R + kGroups3 * kRegion3;                        // [128][LMS] log-mel rows
-  v2f* tw = reinterpret_cast<v2f*>(lm + kLmRows3 * LMS);      // per-lane twiddle table
-  float* dtb = reinterpret_cast<float*>(tw) + 2 * 16 * (kTwaStride + kTwbStride);  // DCT operand table
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = tid >> 4;
-  const int j = tid & 15;
-  stage_twiddles(plan, tw, tid, kThreads3);
-  dct_mfma_setup<SPEC>(plan, dtb, lm, kLmRows3, tid, kThreads3);  // the DCT operand table, zero pad columns
-  LaneConsts L;
-  if constexpr (VAD_M3_TW >= 1) lane_consts(plan, j, L);  // twiddles in VGPRs (all, or stage A's)
-  else lane_ints(j, L);
-  const v4f* twa4 = reinterpret_cast<const v4f*>(tw + j * kTwaStride);
-  const v4f* twb4 = reinterpret_cast<const v4f*>(tw + 16 * kTwaStride + j * kTwbStride);
-
-  // frame-granular balanced runs: workgroup b owns frames [b F / G, (b+1) F / G)
-  const int64_t f_beg = n_frames * blockIdx.x / gridDim.x;
-  const int64_t f_end = n_frames * (blockIdx.x + 1) / gridDim.x;
-  const int64_t t_end = (f_end - f_beg + kTile3 - 1) / kTile3;
-  const int64_t flast = n_frames - 1;
-  v2f* gscr = reinterpret_cast<v2f*>(R + grp * kRegion3);
-  float* prow0 = R + row_off3(grp, 0);
-  float* prow1 = R + row_off3(grp, 1);
-  auto pair_base = [&](int64_t t, int& lim) __attribute__((always_inline)) {
-    const int64_t F = f_beg + t * kTile3 + 2 * grp;
-    lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
-    return src + (F < flast ? F : flast) * (32 * HOPC);
-  };
-  // phase 2a, frame per lane: every wave runs band `wave` of the 12-band
-  // split for frames 0..63 (lane = frame, log-mel row = lane) and for frames
-  // 64..95 (lanes 0..31; lanes 32..63 repeat them into unused rows 96..127)
-  // (addresses recomputed per tile from an opaque copy of the lane index:
-  // hoisted out of the tile loop they would stay live through the FFT)
-  auto opaque = [](int v) __attribute__((always_inline)) {
-    asm volatile("" : "+v"(v));
-    return v;
-  };
-
-  // lifter x DCT of a tile's log-mel rows on the f32 matrix cores, waves
-  // 0..5 one 16-frame block each (log-mel rows 0..95 = the tile's frames)
-  auto dct_store = [&](int64_t pf0) __attribute__((always_inline)) {
-    if constexpr (VAD_M3_DIAG == 5) dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, 0, out);  // stamps in `out`
-    else dct_mfma16<SPEC>(lm, dtb, 16 * wave, lane, pf0, f_end, out);
-  };
-
-  v2f buf[NB];
-  {
-    int lim;
-    const TIN* b0 = pair_base(0, lim);
-    load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
-  }
-  __syncthreads();  // twiddle table staged
-  (void)NC18;
-  int64_t prev_f0 = -1;
-  for (int64_t tile = 0; tile < t_end; ++tile) {
-    unsigned long long st_[12];
-    (void)st_;
-    M3_STAMP(0);
-    const int64_t f0 = f_beg + tile * kTile3;
-    const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
-    int lim, limc;
-    const TIN* nb = pair_base(tile + 1, lim);
-    const TIN* cb = pair_base(tile, limc);
-    (void)cb;
-    if (active) {
-      v2f u[16];
-      float p0k[8], p0n[8];
-      auto stage_a = [&](auto off) __attribute__((always_inline)) {
-        constexpr int OFF = decltype(off)::value;
-        if constexpr (VAD_M3_TW >= 1) stage_a_reg<TIN, NZ, LEN, OFF, NB>(buf, L, j, u);
-        else stage_a_lds<TIN, NZ, LEN, OFF, NB>(buf, twa4, j, u);
-      };
-      // transpose reads + the even / odd half DFTs + split of one pass; `mid`
-      // runs once every read of the pass is issued (pass 1: pass 0's row store)
-      auto finish = [&](float (&pkv)[8], float (&pnv)[8], auto mid) __attribute__((always_inline)) {
-        v2f E[8], O[8];
-        if constexpr (VAD_M3_SPLITREAD) {
-          v2f col[16];
-          read_col(L.cE, gscr, col);
-          __builtin_amdgcn_sched_barrier(0);
-          pk::dft16_even(col, E);
-          __builtin_amdgcn_sched_barrier(0);
-          read_col(L.cO, gscr, col);
-          asm volatile("" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          mid();
-          __builtin_amdgcn_sched_barrier(0);
-          pk::dft16_odd(col, O);
-        } else {
-          v2f col[32];
-          read_b(L, gscr, col);
-          asm volatile("" ::: "memory");
-          __builtin_amdgcn_sched_barrier(0);
-          mid();
-          __builtin_amdgcn_sched_barrier(0);
-          pk::dft16_even(*reinterpret_cast<v2f(*)[16]>(&col[0]), E);
-          pk::dft16_odd(*reinterpret_cast<v2f(*)[16]>(&col[16]), O);
-        }
-        split_pw<VAD_M3_TW >= 2>(L, twb4, E, O, pkv, pnv);
-      };
-      M3_PRIO(3);
-      stage_a(std::integral_constant<int, 0>{});
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (VAD_M3_BUF13) load_chunks<TIN, NZ, NC18, LEN>(cb, limc, j, buf);  // this tile's 13..17
-      else load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
-      __builtin_amdgcn_sched_barrier(0);
-      M3_STAMP(1);
-      store_a(u, gscr, j);
-      __builtin_amdgcn_sched_barrier(0);
-      M3_PRIO(2);
-      finish(p0k, p0n, [] {});
-      __builtin_amdgcn_sched_barrier(0);
-      M3_STAMP(2);
-      M3_PRIO(1);
-      stage_a(std::integral_constant<int, HOPC>{});
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (VAD_M3_BUF13) load_chunks<TIN, 0, NZ, LEN>(nb, lim, j, buf);  // next tile's 0..12
-      else load_chunks<TIN, HOPC, NC18, LEN>(nb, lim, j, buf);
-      __builtin_amdgcn_sched_barrier(0);
-      M3_STAMP(3);
-      store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
-      __builtin_amdgcn_sched_barrier(0);
-      M3_PRIO(0);
-      float p1k[8], p1n[8];
-      // pass 0's row goes into the block once pass 1's transpose reads are issued
-      finish(p1k, p1n, [&] { store_pw(L, p0k, p0n, prow0); });
-      store_pw(L, p1k, p1n, prow1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    M3_STAMP(4);
-    if constexpr (VAD_M3_DIAG == 1) continue;  // diagnostic builds: phase 1 only
-    if (VAD_M3_DIAG != 2 && prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
-    M3_STAMP(5);
-    lds_barrier();  // power rows complete; log-mel rows consumed
-    M3_STAMP(6);
-    if constexpr (VAD_M3_DIAG == 2) {  // diagnostic builds: phase 1 and the barriers only
-      lds_barrier();
-      continue;
-    }
-    // phase 2a: mel + log10, frame per lane
-    {
-      const int ln = opaque(lane);
-      mel12_dispatch<T>(wave, R + row_off3(ln >> 1, ln & 1), lm + ln * LMS);
-      mel12_dispatch<T>(wave, R + row_off3(32 + ((ln & 31) >> 1), ln & 1), lm + (64 + ln) * LMS);
-    }
-    M3_STAMP(7);
-    lds_barrier();  // log-mel rows complete; the blocks free
-    M3_STAMP(8);
-    prev_f0 = f0;
-    if constexpr (VAD_M3_DIAG == 5) {  // stamps of tiles 0..7: [block][wave][tile][16] in `out`
-      unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
-      if (lane == 0 && tile < 8) {
-#pragma unroll
-        for (int k = 0; k < 9; ++k) stamps[(((size_t)blockIdx.x * kW3 + wave) * 8 + tile) * 16 + k] = st_[k];
-      }
-    }
-  }
-  if (prev_f0 >= 0 && wave < 6) dct_store(prev_f0);
-}
-
 static int num_cus();
 
-template <typename TIN, int SPEC>
-static hipError_t launch_mfcc3(const MfccDev* plan, const TIN* src, int64_t n, float* out, hipStream_t st) {
-  const int64_t n_tiles = (n + kTile3 - 1) / kTile3;
-  const int cap = num_cus();  // persistent: one workgroup per CU
-  const int grid = (int)(n_tiles < cap ? n_tiles : cap);
-  constexpr size_t smem = mfcc3_smem_bytes<SPEC>();
-  static_assert(smem <= 160 * 1024, "LDS");
-  static std::atomic<unsigned long long> attr_done{0};
-  const hipError_t e =
-      ensure_dyn_lds(reinterpret_cast<const void*>(&mfcc3_kernel<TIN, SPEC>), (int)smem, attr_done);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((mfcc3_kernel<TIN, SPEC>), dim3(grid), dim3(kThreads3), smem, st, plan, src, n, out);
-  return hipGetLastError();
-}
-
-#ifndef VAD_MFCC3
-#define VAD_MFCC3 0  // 1: the 12-wave mfcc3_kernel for the reference framing (A/B builds)
-#endif
 
 size_t mfcc_smem_bytes() { return kPBytes + kScrBytes + kLmBytes; }  // 157,696 B
 
@@ -1752,15 +1339,11 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
           return launch_t<TIN, MODE, 13, true, 400, 1, D, 5>(plan, src, stride, len, n, out, st);
         return launch_t<TIN, MODE, 13, true, 400, 1, D == 9 || D == 10 ? 0 : D>(plan, src, stride, len, n, out, st);
       }
-      if (stride == 160 && kPairFrames && VAD_MFCC3)  // the reference hop (config.py:22): 3 waves / SIMD
-        return launch_mfcc3<TIN, 1>(plan, src, n, out, st);
       if (stride == 160 && kPairFrames)
         return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2) {
-      if (stride == 160 && kPairFrames && VAD_MFCC3)
-        return launch_mfcc3<TIN, 2>(plan, src, n, out, st);
       if (stride == 160 && kPairFrames)
         return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);

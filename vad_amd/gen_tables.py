@@ -27,7 +27,6 @@ CONFIGS = [
     ("Mel40", 300, 8000, 40, 16000, 13, 22),   # BASELINE.json config 2
 ]
 WAVES = 8          # phase-2a filter bands (one per wave) of mfcc_kernel
-WAVES12 = 12       # phase-2a filter bands of mfcc3_kernel (12 waves, each one band of two frame sets)
 DCT_GROUPS = 4     # phase-2b coefficient groups c = g, g+4, ... (waves 0..3)
 
 
@@ -127,7 +126,6 @@ def emit_code(name, info):
     the persistent tile loop and spill)."""
     los, lens, taps, d, band, dense = info
     out = mel_bands(name, los, lens, dense, band, WAVES, "mel_band_code")
-    out += mel_bands(name, los, lens, dense, bands(lens, WAVES12), WAVES12, "mel_band12_code")
     out += dct_groups(name, d, DCT_GROUPS, "dct_code")
     return "\n".join(out)
 

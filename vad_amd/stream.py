@@ -15,6 +15,14 @@ labels[s] after a step is the class of stream s's window centred three steps
 earlier, or 255 during each stream's first five steps (feed_frame returns
 None for its first five calls, :48-50).
 
+Host I/O (C5's end-to-end rate includes the copies):
+attach_host_io() adds pinned host buffers ``host_inputs`` (K, S, hop) and
+``host_labels`` (K, S); step_host() runs one step from the first to the
+second -- the H2D copy of every stream's new samples, the hop kernel(s), the
+D2H copy of the labels (vad.py:32-59's loop body for S streams at once) --
+and capture(host_io=True) records exactly that into the graph, replayed
+through vad_graph_launch (hipGraphLaunch, no runtime wrapper in between).
+
 Blocks of hops: with hops_per_step=K a step advances every stream by K hops
 (step_block), K x 10 ms of audio per stream, whose new samples sit in the
 static input block ``inputs`` (K, S, hop) and whose labels land in
@@ -68,6 +76,9 @@ class StreamBatch:
         self.labels = self.label_block[K - 1]
         self.scratch = torch.zeros((S, C), dtype=torch.float32, device=dev)
         self.graph = None
+        self.graph_host_io = False
+        self.host_inputs = None
+        self.host_labels = None
 
     def prime(self, carry):
         """Set the last frame_size - hop samples of every stream (S, L-H)."""
@@ -136,10 +147,10 @@ class StreamBatch:
         if new_samples is not None and (new_samples.shape != self.hop_in.shape
                                         or new_samples.dtype != torch.float32 or not new_samples.is_cuda):
             raise ValueError(f"new_samples must be a CUDA float32 tensor of shape {tuple(self.hop_in.shape)}")
-        if self.graph is not None:
+        if self.graph is not None and not self.graph_host_io:
             if new_samples is not None:
                 self.hop_in.copy_(new_samples)
-            self.graph.replay()
+            self._replay()
         elif self.kernel == "hop" and new_samples is not None and new_samples.stride(1) == 1:
             self._body(new_samples)  # read in place: no copy
         else:
@@ -156,23 +167,63 @@ class StreamBatch:
             if new_samples.shape != self.inputs.shape or new_samples.dtype != torch.float32 \
                     or not new_samples.is_cuda:
                 raise ValueError(f"new_samples must be a CUDA float32 tensor of shape {tuple(self.inputs.shape)}")
-            if self.graph is None and self.kernel == "hop" and new_samples.stride(2) == 1:
+            if (self.graph is None or self.graph_host_io) and self.kernel == "hop" and new_samples.stride(2) == 1:
                 self._hop_call(new_samples, self.K, self.label_block)  # read in place
                 return self.label_block
             self.inputs.copy_(new_samples)
-        if self.graph is not None:
-            self.graph.replay()
+        if self.graph is not None and not self.graph_host_io:
+            self._replay()
         else:
             self._block_body()
         return self.label_block
 
-    def capture(self):
+    def attach_host_io(self):
+        """Pinned host buffers for step_host: host_inputs (K, S, hop) fp32,
+        host_labels (K, S) uint8."""
+        if self.host_inputs is None:
+            self.host_inputs = torch.zeros(tuple(self.inputs.shape), dtype=torch.float32, pin_memory=True)
+            self.host_labels = torch.full(tuple(self.label_block.shape), 255, dtype=torch.uint8,
+                                          pin_memory=True)
+        return self.host_inputs, self.host_labels
+
+    def _host_body(self):
+        self.inputs.copy_(self.host_inputs, non_blocking=True)
+        if self.K == 1:
+            self._body()
+        else:
+            self._block_body()
+        self.host_labels.copy_(self.label_block, non_blocking=True)
+
+    def _replay(self):
+        _lib.check(_lib.lib().vad_graph_launch(ctypes.c_void_p(self.graph.raw_cuda_graph_exec()),
+                                               _lib.stream_ptr()), "vad_graph_launch")
+
+    def step_host(self):
+        """One step (K hops) from ``host_inputs`` to ``host_labels``: H2D
+        copy, the hop kernel(s), D2H copy, all on the current stream (the
+        caller synchronises it before reading host_labels).  Replays the
+        graph when capture(host_io=True) recorded one."""
+        if self.host_inputs is None:
+            raise ValueError("attach_host_io() (or capture(host_io=True)) first")
+        if self.graph is not None and self.graph_host_io:
+            self._replay()
+        else:
+            self._host_body()
+        return self.host_labels
+
+    def capture(self, host_io=False):
         """Capture one step (K hops) into a hipGraph (torch.cuda.CUDAGraph);
-        step() / step_block() replay it, reading the static ``inputs``."""
+        step() / step_block() replay it, reading the static ``inputs``.  With
+        host_io the graph also holds the H2D copy from ``host_inputs`` and the
+        D2H copy to ``host_labels`` (replayed by step_host)."""
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         saved = (self.frames.clone(), self.ring.clone(), self.count.clone(), self.label_block.clone())
-        body = self._body if self.K == 1 else self._block_body
+        if host_io:
+            self.attach_host_io()
+            body = self._host_body
+        else:
+            body = self._body if self.K == 1 else self._block_body
         with torch.cuda.stream(s):
             body()  # warm-up (first launch sets kernel attributes)
         torch.cuda.current_stream().wait_stream(s)
@@ -183,4 +234,5 @@ class StreamBatch:
         with torch.cuda.graph(g):
             body()
         self.graph = g
+        self.graph_host_io = bool(host_io)
         return g
