@@ -265,7 +265,6 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     const double a = -2.0 * M_PI * k / 512.0;
     h.tw_b[k] = make_float2((float)cos(a), (float)sin(a));
   }
-  mx_tables(h.mx_a, h.mx_b);
   p->spec = p->table_spec = p->generic() ? 0 : matches_table<Mel26>(h) ? 1 : matches_table<Mel40>(h) ? 2 : 0;
   if (p->generic()) {
     std::vector<double2> tw(fft_n);

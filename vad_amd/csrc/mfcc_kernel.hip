@@ -25,8 +25,6 @@
 //            lifter x DCT of the log-mel rows, stored to the MFCC rows.  It
 //            runs deferred, in the next tile after phase 1, on the waves that
 //            finish their FFT first -- two barriers per tile.
-#include <string.h>
-
 #include <type_traits>
 
 #include "vad_common.h"
@@ -409,7 +407,7 @@ constexpr int kDctGroups = 4;  // phase 2b: waves 0..3, coefficients c = w, w+4,
 // Phase 2a (runtime plan): frame `lane`, filters [fb, fe) -> log-mel row.
 __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
                                         const float* __restrict__ prow, int fb, int fe,
-                                        float* __restrict__ lrow, int ek = 0) {
+                                        float* __restrict__ lrow) {
   const float eps = 0x1p-52f;  // np.finfo(float).eps, mfcc.py:74
   for (int m = fb; m < fe; ++m) {
     const int lo = plan->f_lo[m], n = plan->f_len[m];
@@ -424,7 +422,7 @@ __device__ __forceinline__ void mel_log(const MfccDev* __restrict__ plan,
       e3 = fmaf(w[t + 3], pr[t + 3], e3);
     }
     for (; t < n; ++t) e0 = fmaf(w[t], pr[t], e0);
-    float e = __builtin_ldexpf((e0 + e1) + (e2 + e3), ek);
+    float e = (e0 + e1) + (e2 + e3);
     e = (e == 0.f) ? eps : e;
     lrow[m] = log10_pos(e);
   }
@@ -461,43 +459,24 @@ __device__ __forceinline__ void dct_rt(const MfccDev* __restrict__ plan,
 // coefficient group G.
 template <class T, int W>
 __device__ __forceinline__ void mel_band_code(const float* __restrict__ prow,
-                                              float* __restrict__ lm, int ek);
-// the same over the matrix-core kernel's power rows (columns permuted, mfcc_mx.h)
-template <class T, int W>
-__device__ __forceinline__ void mel_band_code_mx(const float* __restrict__ prow,
-                                                 float* __restrict__ lm, int ek);
+                                              float* __restrict__ lm);
 template <class T, int G>
 __device__ __forceinline__ void dct_code(const float* __restrict__ lm, float (&acc)[4]);
 
 #include "mel_code.h"
 
 template <class T>
-__device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float* lrow, int ek) {
+__device__ __forceinline__ void mel_dispatch(int wave, const float* prow, float* lrow) {
   prow = static_cast<const float*>(__builtin_assume_aligned(prow, 16));
   switch (wave) {
-    case 0: mel_band_code<T, 0>(prow, lrow, ek); break;
-    case 1: mel_band_code<T, 1>(prow, lrow, ek); break;
-    case 2: mel_band_code<T, 2>(prow, lrow, ek); break;
-    case 3: mel_band_code<T, 3>(prow, lrow, ek); break;
-    case 4: mel_band_code<T, 4>(prow, lrow, ek); break;
-    case 5: mel_band_code<T, 5>(prow, lrow, ek); break;
-    case 6: mel_band_code<T, 6>(prow, lrow, ek); break;
-    default: mel_band_code<T, 7>(prow, lrow, ek); break;
-  }
-}
-
-template <class T>
-__device__ __forceinline__ void mel_dispatch_mx(int wave, const float* prow, float* lrow, int ek) {
-  prow = static_cast<const float*>(__builtin_assume_aligned(prow, 16));
-  switch (wave) {
-    case 0: mel_band_code_mx<T, 0>(prow, lrow, ek); break;
-    case 1: mel_band_code_mx<T, 1>(prow, lrow, ek); break;
-    case 2: mel_band_code_mx<T, 2>(prow, lrow, ek); break;
-    case 3: mel_band_code_mx<T, 3>(prow, lrow, ek); break;
-    case 4: mel_band_code_mx<T, 4>(prow, lrow, ek); break;
-    case 5: mel_band_code_mx<T, 5>(prow, lrow, ek); break;
-    case 6: mel_band_code_mx<T, 6>(prow, lrow, ek); break;
-    default: mel_band_code_mx<T, 7>(prow, lrow, ek); break;
+    case 0: mel_band_code<T, 0>(prow, lrow); break;
+    case 1: mel_band_code<T, 1>(prow, lrow); break;
+    case 2: mel_band_code<T, 2>(prow, lrow); break;
+    case 3: mel_band_code<T, 3>(prow, lrow); break;
+    case 4: mel_band_code<T, 4>(prow, lrow); break;
+    case 5: mel_band_code<T, 5>(prow, lrow); break;
+    case 6: mel_band_code<T, 6>(prow, lrow); break;
+    default: mel_band_code<T, 7>(prow, lrow); break;
   }
 }
 
@@ -513,28 +492,15 @@ __device__ __forceinline__ void dct_dispatch(int g, const float* lrow, float (&a
 }
 
 // Phase 2a: one frame per lane, wave `wave` owns a band of filters: mel
-// energies (x 2^ek: the matrix-core kernel's per-tile scale; 0 elsewhere),
-// (==0 -> eps), log10 into the tile's log-mel rows.
+// energies, (==0 -> eps), log10 into the tile's log-mel rows.
 template <int SPEC>
 __device__ __forceinline__ void phase2a(const MfccDev* __restrict__ plan, const float* P,
-                                        float* lm, int wave, int lane, int ek = 0) {
+                                        float* lm, int wave, int lane) {
   const float* prow = P + lane * kPStride;
   float* lrow = lm + lane * lm_stride<SPEC>();
-  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow, ek);
-  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow, ek);
-  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow, ek);
-}
-
-// phase 2a of the matrix-core kernel: the compiled banks read its permuted
-// power rows; the runtime taps read plain rows (PERM false)
-template <int SPEC>
-__device__ __forceinline__ void phase2a_mx(const MfccDev* __restrict__ plan, const float* P, float* lm, int wave,
-                                           int lane, int ek) {
-  const float* prow = P + lane * kPStride;
-  float* lrow = lm + lane * lm_stride<SPEC>();
-  if constexpr (SPEC == 1) mel_dispatch_mx<Mel26>(wave, prow, lrow, ek);
-  else if constexpr (SPEC == 2) mel_dispatch_mx<Mel40>(wave, prow, lrow, ek);
-  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow, ek);
+  if constexpr (SPEC == 1) mel_dispatch<Mel26>(wave, prow, lrow);
+  else if constexpr (SPEC == 2) mel_dispatch<Mel40>(wave, prow, lrow);
+  else mel_log(plan, prow, plan->wave_fbeg[wave], plan->wave_fend[wave], lrow);
 }
 
 // Phase 2b (waves 0..3): lifter x DCT of the tile's log-mel rows, one frame
@@ -679,8 +645,6 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
-
-#include "mfcc_mx.h"
 
 // DIAG (diagnostic library builds only: `python -m vad_amd.build --variant NAME
 // -DVAD_DIAG_BUILD=n`, never the shipped libvad_amd.so): 5/6 timestamps, 7 an
@@ -1343,127 +1307,10 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
   return hipGetLastError();
 }
 
-// ---- matrix-core kernel (mfcc_mx.h): operand images and launch ----
-// f16 round-to-nearest-even of a double (via float, then the neighbour that
-// is nearer to the double: no double rounding)
-static uint16_t f16_bits(double v) {
-  const _Float16 h = (_Float16)(float)v;
-  uint16_t b;
-  memcpy(&b, &h, 2);
-  double err = fabs((double)(float)h - v);
-  for (int d = -1; d <= 1; d += 2) {
-    const uint16_t c = (uint16_t)(b + d);
-    _Float16 hc;
-    memcpy(&hc, &c, 2);
-    const double e = fabs((double)(float)hc - v);
-    if (e < err || (e == err && (c & 1) == 0 && (b & 1))) { err = e; b = c; }
-  }
-  return b;
-}
-static double f16_val(uint16_t b) {
-  _Float16 h;
-  memcpy(&h, &b, 2);
-  return (double)(float)h;
-}
-// A-operand image of a 16 x 32 matrix M[row][k] for v_mfma_f32_16x16x32_f16:
-// lane (g, i) holds row i, k = 8 g + j in f16 element j; hi image then lo
-// image (lo = f16(v - hi)), 256 dwords each
-static void mx_image(const double (&M)[16][32], uint32_t* out) {
-  for (int lane = 0; lane < 64; ++lane) {
-    const int g = lane >> 4, i = lane & 15;
-    for (int d = 0; d < 4; ++d) {
-      const double a = M[i][8 * g + 2 * d], b = M[i][8 * g + 2 * d + 1];
-      const uint16_t ha = f16_bits(a), hb = f16_bits(b);
-      const uint16_t la = f16_bits(a - f16_val(ha)), lb = f16_bits(b - f16_val(hb));
-      out[lane * 4 + d] = ha | ((uint32_t)hb << 16);
-      out[256 + lane * 4 + d] = la | ((uint32_t)lb << 16);
-    }
-  }
-}
-void mx_tables(uint32_t* a, uint32_t* b) {
-  // stage A, rows p = 16 t + i (p = 2 kp + re|im; p = 1: Re A[16]), k = n1
-  for (int t = 0; t < 2; ++t) {
-    double M[16][32];
-    for (int i = 0; i < 16; ++i)
-      for (int n1 = 0; n1 < 32; ++n1) {
-        const int p = 16 * t + i, kp = p >> 1;
-        double v;
-        if (n1 >= 25) v = 0.0;  // 16 n1 + n2 >= 400: zero padding
-        else if (p == 1) v = (n1 & 1) ? -1.0 : 1.0;  // W32^(16 n1)
-        else {
-          const double th = 2.0 * M_PI * n1 * kp / 32.0;
-          v = (p & 1) ? -sin(th) : cos(th);
-        }
-        M[i][n1] = v;
-      }
-    mx_image(M, a + t * 512);
-  }
-  // stage B, matrix m = kp (0..15) and m = 16 (the bins 16 + 32 k2 from
-  // kp = 0's data): rows (k2, re|im), k = (n2, re|im) of A[n2][kp]
-  for (int m = 0; m < 17; ++m) {
-    double M[16][32];
-    memset(M, 0, sizeof(M));
-    for (int k2 = 0; k2 < 8; ++k2)
-      for (int n2 = 0; n2 < 16; ++n2) {
-        const double th = 2.0 * M_PI * n2 * ((m == 16 ? 16 : m) + 32 * k2) / 512.0;
-        const double c = cos(th), sn = -sin(th);
-        if (m == 0) {  // A[n2][0] real
-          M[2 * k2][2 * n2] = c;
-          M[2 * k2 + 1][2 * n2] = sn;
-        } else if (m == 16) {  // A[n2][16] real, in the Im slot of kp = 0; rows k2 = 7 - slot
-          M[2 * (7 - k2)][2 * n2 + 1] = c;
-          M[2 * (7 - k2) + 1][2 * n2 + 1] = sn;
-        } else {  // complex multiply (c + i sn)(re + i im)
-          M[2 * k2][2 * n2] = c;
-          M[2 * k2][2 * n2 + 1] = -sn;
-          M[2 * k2 + 1][2 * n2] = sn;
-          M[2 * k2 + 1][2 * n2 + 1] = c;
-        }
-      }
-    mx_image(M, b + m * 512);
-  }
-}
-
-template <typename TIN, int SPEC, bool V4>
-static hipError_t launch_mx_t(const MfccDev* plan, const TIN* src, int64_t n, float* out, hipStream_t st,
-                              const MfccBalance& bal) {
-  const int64_t n_tiles = (n + kTile - 1) / kTile;
-  const int cap = num_cus();  // persistent, LDS-bound: one workgroup per CU
-  const int grid = (int)(n_tiles < cap ? n_tiles : cap);
-  static std::atomic<unsigned long long> attr_done{0};
-  const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&mfcc_mx_kernel<TIN, SPEC, V4>),
-                                      (int)mx::kSmemBytes, attr_done);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((mfcc_mx_kernel<TIN, SPEC, V4>), dim3(grid), dim3(kThreads), mx::kSmemBytes, st, plan, src, n,
-                     out, bal);
-  return hipGetLastError();
-}
-
-template <typename TIN>
-static hipError_t launch_mx(const MfccDev* plan, int spec, const TIN* src, int64_t n, float* out, hipStream_t st,
-                            const MfccBalance& bal) {
-  const bool v4 = reinterpret_cast<uintptr_t>(src) % (4 * sizeof(TIN)) == 0;
-  if (spec == 1) return v4 ? launch_mx_t<TIN, 1, true>(plan, src, n, out, st, bal)
-                           : launch_mx_t<TIN, 1, false>(plan, src, n, out, st, bal);
-  if (spec == 2) return v4 ? launch_mx_t<TIN, 2, true>(plan, src, n, out, st, bal)
-                           : launch_mx_t<TIN, 2, false>(plan, src, n, out, st, bal);
-  return v4 ? launch_mx_t<TIN, 0, true>(plan, src, n, out, st, bal)
-            : launch_mx_t<TIN, 0, false>(plan, src, n, out, st, bal);
-}
-
-#ifndef VAD_MFCC_MX
-#define VAD_MFCC_MX 1  // 0 (A/B builds): the reference framing runs the VALU-FFT kernel
-#endif
-
 template <typename TIN, int MODE>
 static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st, const MfccBalance& bal = MfccBalance()) {
   const int used = len < kFftN ? len : kFftN;
-  // the reference framing (config.py:21) without an analysis window: the
-  // matrix-core kernel
-  if (VAD_MFCC_MX && VAD_DIAG_BUILD == 0 && MODE == kAudioToMfcc && len == 400 && stride == 160 &&
-      (spec == 0 || spec == 1 || spec == 2))
-    return launch_mx<TIN>(plan, spec, src, n, out, st, bal);
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
                     ((stride & 1) == 0) && ((used & 1) == 0);
   if ((spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40) && used == 400 && vec2 &&

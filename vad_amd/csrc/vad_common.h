@@ -35,14 +35,7 @@ struct MfccDev {
   float2 tw_a[256];                  // W256^(n2*k1), [n2][k1]
   float2 tw_b[256];                  // W512^k
   float window[kFftN];               // optional analysis window (kSpecWindow plans), 0 past the frame
-  // matrix-core DFT operand images (mfcc_mx.h), [m][hi | lo][lane][4 dwords]
-  // of split-f16 16 x 32 matrices: stage A (2 row halves), stage B (17)
-  uint32_t mx_a[2 * 2 * 64 * 4];
-  uint32_t mx_b[17 * 2 * 64 * 4];
 };
-
-// fills MfccDev::mx_a / mx_b (mfcc_kernel.hip)
-void mx_tables(uint32_t* a, uint32_t* b);
 
 // plan variant of a plan with an analysis window (vad_mfcc_plan_set_window)
 constexpr int kSpecWindow = 3;

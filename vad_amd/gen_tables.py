@@ -126,39 +126,26 @@ def emit_code(name, info):
     the persistent tile loop and spill)."""
     los, lens, taps, d, band, dense = info
     out = mel_bands(name, los, lens, dense, band, WAVES, "mel_band_code")
-    out += mel_bands(name, los, lens, dense, band, WAVES, "mel_band_code_mx", col=mx_col)
     out += dct_groups(name, d, DCT_GROUPS, "dct_code")
     return "\n".join(out)
 
 
-def mx_col(k):
-    """Power-row column of bin k in the matrix-core kernel (mfcc_mx.h): the
-    upper half of every 32-bin block is rotated by one (bin 32 m + 16 + u at
-    column 32 m + 16 + (u - 1 mod 16)), so that each wave's mirror bins form
-    aligned runs of eight."""
-    u = k & 15
-    return (k & ~31) | ((16 + ((u + 15) & 15)) if k & 16 else u)
-
-
-def mel_bands(name, los, lens, dense, band, waves, fname, col=lambda k: k):
+def mel_bands(name, los, lens, dense, band, waves, fname):
     out = []
     comp = "xyzw"
     for w in range(waves):
         fb, fe = band[w], band[w + 1]
         out.append(f"template <> __device__ __forceinline__ void {fname}<{name}, {w}>(")
-        out.append("    const float* __restrict__ prow, float* __restrict__ lm, int ek) {")
+        out.append("    const float* __restrict__ prow, float* __restrict__ lm) {")
         if fb == fe:
-            out.append("  (void)prow;\n  (void)lm;\n  (void)ek;\n}")
+            out.append("  (void)prow;\n  (void)lm;\n}")
             continue
         k0 = los[fb] & ~3
         k1 = los[fe - 1] + lens[fe - 1]
-        # the 16-B chunks of the power row holding the band's bins (columns
-        # col(k)), read once each
-        chunks = sorted({col(k) >> 2 for k in range(k0, k1)})
-        qi = {c: i for i, c in enumerate(chunks)}
-        for q, c in enumerate(chunks):
+        nq = (k1 - k0 + 3) // 4
+        for q in range(nq):
             out.append(f"  const v4f q{q} = *reinterpret_cast<const v4f*>("
-                       f"__builtin_assume_aligned(prow + {4 * c}, 16));")
+                       f"__builtin_assume_aligned(prow + {k0 + 4 * q}, 16));")
         # each filter's taps split into two interleaved sub-chains, all chains
         # of the band emitted round-robin (volatile: the order is the issue
         # order), so that no fmac consumes the accumulator written by the
@@ -176,7 +163,7 @@ def mel_bands(name, los, lens, dense, band, waves, fname, col=lambda k: k):
                 if step >= len(t):
                     continue
                 k, v = t[step]
-                q, r = qi[col(k) >> 2], col(k) & 3
+                q, r = divmod(k - k0, 4)
                 src = f"q{q}.{comp[r]}"
                 if step == 0:
                     out.append(f'  asm volatile("v_mul_f32_e32 %0, {bits(v)}, %1" : "=v"({reg}) : "v"({src}));')
@@ -184,9 +171,7 @@ def mel_bands(name, los, lens, dense, band, waves, fname, col=lambda k: k):
                     out.append(f'  asm volatile("v_fmac_f32_e32 %0, {bits(v)}, %1" : "+v"({reg}) : "v"({src}));')
         for m in range(fb, fe):
             regs = [reg for reg, _ in chains if reg.startswith(f"e{m - fb}_")]
-            # x 2^ek: the matrix-core kernel's power rows carry a per-tile
-            # power-of-two scale (exact; ek = 0 folds away in the others)
-            out.append(f"  const float e{m - fb} = __builtin_ldexpf({' + '.join(regs)}, ek);")
+            out.append(f"  const float e{m - fb} = {' + '.join(regs)};")
         for m in range(fb, fe):
             out.append(f"  lm[{m}] = log10_pos(e{m - fb} == 0.f ? 0x1p-52f : e{m - fb});"
                        f"  // (==0 -> eps), log10")
