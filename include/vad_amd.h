@@ -148,7 +148,13 @@ int vad_ffn_plan_set_arith(vad_ffn_plan* plan, int32_t arith);
  *   mode VAD_FEAT_OFFLINE: [Mc, M+1 - M-1, (M+2 - Mc) - (Mc - M-2)], no
  *     normalisation (dataset/file_processing.py:40-70).
  * Row i is centred on MFCC frame i+2, i = 0..n_frames-6 (F-5 rows; the last
- * full window is never emitted, exactly as both reference loops do). */
+ * full window is never emitted, exactly as both reference loops do).
+ * Supported range (analyser mode): the normalisation is fp32, v_rsq_f32 on
+ * 0.2 * var * 2^24.  For caller-supplied rows whose 5-frame std lies in
+ * [2^-60, 2^50] Mn is the fp32 formula's (log-MFCCs of any audio are far
+ * inside); past ~2^52 the scaled variance overflows and Mn = 0, below ~2^-75
+ * the squares underflow and Mn = +-inf, where the reference's fp64 gives a
+ * finite value (tests/test_gpu_parity.py::test_feature_range_edges). */
 #define VAD_FEAT_ANALYSER 0
 #define VAD_FEAT_OFFLINE 1
 

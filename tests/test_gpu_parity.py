@@ -998,3 +998,36 @@ def test_nonfinite_samples(torch_cuda):
         x = O.analyser_features_fast(ref)[:, :13]
         sure = O.ffn_margin(x, layers) > MARGIN_TOL
     np.testing.assert_array_equal(labels[sure & ~win_bad], O.ffn_labels(x, layers)[sure & ~win_bad])
+
+
+@pytest.mark.gpu
+def test_feature_range_edges(torch_cuda):
+    """The analyser normalisation is fp32 with v_rsq_f32 on 0.2 var 2^24
+    (features.h): caller-supplied MFCC rows whose 5-frame std lies in
+    [2^-60, 2^50] give the oracle's Mn (and deltas) to fp32 rounding; past
+    that the documented edges hold (include/vad_amd.h, vad_features_f32):
+    std ~2^56 overflows the scaled variance -> Mn = 0, std ~2^-90 underflows
+    the squares -> Mn = +-inf.  Log-MFCCs of any audio sit far inside."""
+    torch = torch_cuda
+    from vad_amd.plan import window_features
+    rng = np.random.default_rng(7)
+    base = rng.standard_normal((64, 13)).astype(np.float32)
+    for k in (-60, -30, 0, 20, 50):
+        m = (base * np.float32(2.0 ** k)).astype(np.float32)
+        got = window_features(torch.from_numpy(m).cuda()).cpu().numpy().astype(np.float64)
+        ref = O.analyser_features_fast(m)
+        assert np.isfinite(got).all(), k
+        np.testing.assert_allclose(got[:, :13], ref[:, :13], rtol=1e-5, atol=1e-5, err_msg=f"Mn at 2^{k}")
+        scale = 2.0 ** k
+        np.testing.assert_allclose(got[:, 13:26] / scale, ref[:, 13:26] / scale, rtol=0, atol=1e-5,
+                                   err_msg=f"M+1 - M-1 at 2^{k}")
+        # (M+2 - Mn) - (Mn - M-2) mixes the O(1) Mn with rows at the scale
+        np.testing.assert_allclose(got[:, 26:], ref[:, 26:], rtol=1e-5, atol=1e-5 * max(1.0, scale),
+                                   err_msg=f"second deltas at 2^{k}")
+    hi = (base * np.float32(2.0 ** 56)).astype(np.float32)
+    got = window_features(torch.from_numpy(hi).cuda()).cpu().numpy()
+    assert (got[:, :13] == 0).all()  # scaled variance overflows: rsq(inf) = 0
+    assert np.isfinite(got[:, 13:26]).all()  # M+1 - M-1 unaffected
+    lo = (base * np.float32(2.0 ** -90)).astype(np.float32)
+    got = window_features(torch.from_numpy(lo).cuda()).cpu().numpy()
+    assert np.isinf(got[:, :13]).all()  # squares underflow: var 0, e2 / 0

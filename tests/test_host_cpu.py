@@ -65,22 +65,23 @@ def test_abi_rejects_invalid_arguments():
 
 
 def test_shipped_library_has_no_diagnostic_kernels():
-    """Diagnostic kernel instantiations (timestamps in place of MFCCs, an
-    L2-resident source, phase-1-only timing) exist only in libraries built
-    with -DVAD_DIAG_BUILD=n; the shipped library has none and reads no
-    environment variable that could select one."""
+    """The diagnostic instrumentation of rounds 1-3 (timestamps in place of
+    MFCCs, an L2-resident source, phase-1-only timing) was removed from the
+    kernels in round 4: mfcc_kernel has no DIAG template parameter any more
+    (<TIN, MODE, NZ, VEC2, LEN, SPEC, HOPC, WIN>) and the library reads no
+    environment variable that could select a diagnostic path."""
     import re
     import subprocess
     from vad_amd import _lib
     data = open(_lib.LIB_PATH, "rb").read()
-    assert b"VAD_DIAG" not in data and b"VAD_FFN_EXACT" not in data
+    assert b"VAD_DIAG" not in data and b"VAD_FFN_EXACT" not in data and b"VAD_MFCC_CUS" not in data
     syms = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
                           check=True).stdout + subprocess.run(["nm", _lib.LIB_PATH], capture_output=True,
                                                               text=True).stdout
-    # mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC>
-    diag = re.findall(r"mfcc_kernelI[fs]Li\d+ELi\d+ELb\dELi\d+ELi\d+ELi(\d+)ELi\d+E", syms)
-    assert diag, "mfcc_kernel instantiations not found in the symbol table"
-    assert set(diag) == {"0"}, sorted(set(diag))
+    # host stubs of mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, HOPC, WIN>: exactly 8 template arguments
+    inst = re.findall(r"mfcc_kernelI[fs](?:L[ib]\d+E){7}EEv", syms)
+    assert inst, "mfcc_kernel instantiations not found in the symbol table"
+    assert not re.findall(r"mfcc_kernelI[fs](?:L[ib]\d+E){8}EEv", syms)
 
 
 def test_stream_ring_size():

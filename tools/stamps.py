@@ -1,4 +1,5 @@
-"""Phase timing of mfcc_kernel from in-kernel s_memtime stamps (a -DVAD_DIAG_BUILD=5 library)."""
+"""[Historical: the diagnostic hooks this needs were removed from the shipped kernels in round 4;
+build it from a tree at or before commit 4f8ce33.]  Phase timing of mfcc_kernel from in-kernel s_memtime stamps (a -DVAD_DIAG_BUILD=5 library)."""
 import os
 import sys
 

@@ -1,4 +1,5 @@
-"""Phase timing of mfcc3_kernel from in-kernel s_memtime stamps (a -DVAD_MFCC3=1 -DVAD_M3_DIAG=5 build):
+"""[Historical: the diagnostic hooks this needs were removed from the shipped kernels in round 4;
+build it from a tree at or before commit 4f8ce33.]  Phase timing of mfcc3_kernel from in-kernel s_memtime stamps (a -DVAD_MFCC3=1 -DVAD_M3_DIAG=5 build):
 VAD_AMD_LIB=... python tools/stamps3.py"""
 import os
 import sys

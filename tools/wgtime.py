@@ -1,4 +1,5 @@
-"""Per-workgroup start/end stamps of mfcc_kernel (a -DVAD_DIAG_BUILD=9 library): shader clock,
+"""[Historical: the diagnostic hooks this needs were removed from the shipped kernels in round 4;
+build it from a tree at or before commit 4f8ce33.]  Per-workgroup start/end stamps of mfcc_kernel (a -DVAD_DIAG_BUILD=9 library): shader clock,
 workgroup durations vs kernel wall time, dispatch skew."""
 import os
 import sys

@@ -39,7 +39,10 @@ __device__ __forceinline__ Feat3 feature_triple(float a0, float a1, float a2, fl
     // operations per item); the 2^12 goes back into e2 exactly.  For every
     // normal var the result is rsqrtf's bit for bit (v_rsq_f32(x 2^24) 2^12
     // == v_rsq_f32(x) over all 1.93e9 normal x below 2^104 on gfx950,
-    // tools/checks/rsq_scale_check.hip)
+    // tools/checks/rsq_scale_check.hip).  Range edges (documented at
+    // vad_features_f32, locked by test_feature_range_edges): a var whose
+    // scaled value overflows (std past ~2^52) gives Mn = 0, squares that
+    // underflow (std below ~2^-75) give Mn = +-inf
     const float var_s = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * (0.2f * 0x1p24f);
     const bool flat = (a0 == a1) & (a1 == a2) & (a2 == a3) & (a3 == a4);
     // branch-free: the NaN is added in rather than selected around the rsqrt

@@ -7,9 +7,6 @@
 #include "vad_common.h"
 #include "features.h"
 
-#ifndef VAD_FFN_DIAG
-#define VAD_FFN_DIAG 0  // diagnostic builds only: 1 skips the features, 2 the MLP
-#endif
 
 namespace vad {
 
@@ -579,7 +576,7 @@ __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, 
 #pragma unroll
   for (int r = 0; r < (kWTile * MN + 63) / 64; ++r) {
     const int it = lane + 64 * r;
-    if ((r < kWTile * MN / 64 || it < kWTile * MN) && VAD_FFN_DIAG != 1) {
+    if (r < kWTile * MN / 64 || it < kWTile * MN) {
       const int w = it / MN, c = it - MN * w;
       const Feat3 ft = feature_triple(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
                                       R[it + 4 * MN], MODE);
@@ -652,8 +649,7 @@ template <int KS0, int T1, int T2, int T3, int T4, int NC, bool NOVL, bool IN_BO
           class FV>
 __device__ __forceinline__ int wave_tile_mlp(float (&x0)[(4 * KS0 + 31) / 32][8], int wnan, FH fh, FB fb, FV fv,
                                              int n_classes, f32x4& z) {
-  if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
-  else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, FB, FV, NOVL, IN_BOUNDED>(fh, fb, fv, x0);
+  z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC, FB, FV, NOVL, IN_BOUNDED>(fh, fb, fv, x0);
   if (wnan) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
   return argmax_classes(z, n_classes);
 }

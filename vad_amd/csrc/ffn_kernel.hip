@@ -188,7 +188,7 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
       // eight rows 4q .. 4q+7 they span (all loads issued at once); windows
       // past nwin read rows past the clip (zero-filled): written, not used
       const int c = tid % MN, q = tid / MN;
-      if (q < kChunk / 4 && VAD_FFN_DIAG != 1) {
+      if (q < kChunk / 4) {
         float a[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] = rw_[(4 * q + k) * MN + c];
@@ -216,7 +216,7 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
         }
       }
     } else
-    for (int i = tid; i < (VAD_FFN_DIAG == 1 ? 0 : nwin * mfcc_n); i += 256) {
+    for (int i = tid; i < nwin * mfcc_n; i += 256) {
       const int w = i / mfcc_n, c = i - w * mfcc_n;
       constexpr int kRS = MN > 0 ? MN : kMaxCoefs;  // row stride of the staged rows
       const float* r = rw_ + w * kRS + c;
@@ -257,8 +257,7 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
         for (int q = 0; q < 8; ++q)
           if (8 + q >= 13) x0[0][q] = 8 * (g & 1) + q < 13 ? x0[0][q] : 0.f;
       }
-      if (VAD_FFN_DIAG == 2) z = (f32x4){x0[0][0], x0[0][1], 0.f, 0.f};
-      else z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(FragRegs{fh}, (const float*)fb, (const float*)fv, x0);
+      z = mlp_forward_h3<KS0, T1, T2, T3, T4, NC>(FragRegs{fh}, (const float*)fb, (const float*)fv, x0);
       if (wnan[buf][wl]) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
     } else {
       float x[KS0];

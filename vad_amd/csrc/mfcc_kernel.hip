@@ -48,37 +48,13 @@ enum Mode { kAudioToMfcc = 0, kAudioToSpec = 1, kSpecToMfcc = 2 };
 // Sample loads by input type: fp32, or int16 PCM (the reference reads int16
 // audio and converts with astype(float32), vad.py:37 / file_processing.py:26-35;
 // the conversion is exact, so both inputs give identical spectra).
-#ifndef VAD_NO_STORE
-#define VAD_NO_STORE 0  // diagnostic builds only: MFCC results are not written
-#endif
-#ifndef VAD_DIAG_BUILD
-#define VAD_DIAG_BUILD 0  // 0 in the shipped library: no diagnostic kernel is instantiated
-#endif
-#ifndef VAD_NT_LOADS
-#define VAD_NT_LOADS 0
-#endif
-#ifndef VAD_DCT_AT
-#define VAD_DCT_AT 0  // where the paired-frame loop runs the deferred DCT (A/B builds): 0 waves 0..3
-                      // after phase 1, 1 waves 0..3 before it, 2 waves 4..7 after it
-#endif
-#ifndef VAD_DIAG_XP
-#define VAD_DIAG_XP 0  // diagnostic builds (VAD_DIAG_BUILD=10) only: see the paired-frame phase 1
-#endif
 template <typename TIN>
 struct Samples;
 template <>
 struct Samples<float> {
   static constexpr int kPairAlign = 8;  // bytes for one aligned 2-sample load
   __device__ static v2f pair(const float* p) {
-#if VAD_NT_LOADS == 2
-    const unsigned long long b = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p),
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_bit_cast(v2f, b);
-#elif VAD_NT_LOADS
-    return __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p));
-#else
     return *reinterpret_cast<const v2f*>(p);
-#endif
   }
   __device__ static float one(const float* p) { return *p; }
   __device__ static v2f raw_pair(const float* p) { return pair(p); }
@@ -89,11 +65,7 @@ template <>
 struct Samples<int16_t> {
   static constexpr int kPairAlign = 4;
   __device__ static v2f pair(const int16_t* p) {
-#if VAD_NT_LOADS
-    const int v = __builtin_nontemporal_load(reinterpret_cast<const int*>(p));
-#else
     const int v = *reinterpret_cast<const int*>(p);
-#endif
     return (v2f){(float)(int16_t)(v & 0xffff), (float)(v >> 16)};
   }
   __device__ static float one(const int16_t* p) { return (float)*p; }
@@ -102,11 +74,7 @@ struct Samples<int16_t> {
   // (the loads sit in sched_barrier-fenced regions), which serialised the
   // one-tile-ahead prefetch of the int16 kernel
   __device__ static v2f raw_pair(const int16_t* p) {
-#if VAD_NT_LOADS
-    const int v = __builtin_nontemporal_load(reinterpret_cast<const int*>(p));
-#else
     const int v = *reinterpret_cast<const int*>(p);
-#endif
     return (v2f){__builtin_bit_cast(float, v), 0.f};
   }
   __device__ static v2f raw_two(const int16_t* p0, const int16_t* p1) {
@@ -126,14 +94,6 @@ struct Samples<int16_t> {
 // pad_stage_a, at first use.  LEN > 0 fixes the frame length at compile time
 // (400 for clips); VEC2 (pair-aligned frames of even length) loads a sample
 // pair per load.
-#ifndef VAD_SPLIT_LOADS
-#define VAD_SPLIT_LOADS 1
-#endif
-constexpr bool kSplitLoads = VAD_SPLIT_LOADS != 0;
-#ifndef VAD_PAIR_FRAMES
-#define VAD_PAIR_FRAMES 1
-#endif
-constexpr bool kPairFrames = VAD_PAIR_FRAMES != 0;
 
 template <typename TIN, int NZ, bool VEC2, int LEN, int B = 0, int E = NZ>
 __device__ __forceinline__ void load_stage_a(const TIN* __restrict__ fr, int len_rt, int n2,
@@ -584,23 +544,6 @@ __device__ __forceinline__ void phase2b_any(const MfccDev* __restrict__ plan, co
   else phase2b<SPEC, STORE>(plan, lm, wave, lane, f0, n_frames, mfcc_n, out);
 }
 
-// In-kernel timestamps for DIAG 5/6 (diagnostic builds only): every wave
-// takes s_memtime at phase boundaries into SGPRs; lane 0 stores them at the
-// end of each of its first 8 tiles into `out` as [block][wave][tile][16]
-// (deferred, so that the stamps add no lgkmcnt waits inside the tile; the
-// MFCC stores are suppressed).  DIAG 6 idles waves 4..7 (barriers only) to
-// time the older waves' phases alone.
-#define VAD_STAMP(k)                                                              \
-  do {                                                                            \
-    if constexpr (DIAG == 5 || DIAG == 6) {                                       \
-      __builtin_amdgcn_sched_barrier(0);                                          \
-      st_[k] = __builtin_amdgcn_s_memtime();                                      \
-      __builtin_amdgcn_sched_barrier(0);                                          \
-    }                                                                             \
-  } while (0)
-constexpr int kStamps = 11;
-
-
 // Milestone priorities (paired-frame loop, fp32 input): a wave lowers its
 // issue priority (s_setprio 3 -> 0) each time it passes a phase-1 milestone
 // (tile start, pass-0 transpose issued, pass-1 stage A, pass-0 power row),
@@ -609,11 +552,8 @@ constexpr int kStamps = 11;
 // closer together: -7 us per 1M frames on fp32 input; on int16 input -4 us
 // since its samples are converted at first use (before that, with the
 // prefetch serialised by the conversion, +3.5 us).
-#ifndef VAD_PRIO_I16
-#define VAD_PRIO_I16 1
-#endif
 template <typename TIN>
-constexpr bool kMilestonePrio = std::is_same_v<TIN, float> || VAD_PRIO_I16;
+constexpr bool kMilestonePrio = true;
 
 // (Placements measured: 3/2/1/0 at these four; 3/2/-/1 + 0 after the pass-1
 // power row +4 us; 3/-/2/1 + 0 there the same.  Spreading the DCT over all
@@ -646,11 +586,11 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// DIAG (diagnostic library builds only: `python -m vad_amd.build --variant NAME
-// -DVAD_DIAG_BUILD=n`, never the shipped libvad_amd.so): 5/6 timestamps, 7 an
-// L2-resident source, 9 per-workgroup stamps, 10 phase 1 only -- outputs wrong.
 // HOPC > 0 (LEN > 0, VEC2, hop = 32 HOPC samples): paired-frame phase 1.
-template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int DIAG = 0, int HOPC = 0, bool WIN = false>
+// (The diagnostic instrumentation of earlier rounds -- in-kernel stamps,
+// phase-1-only and L2-resident-source builds -- lives in git history before
+// round 4; DESIGN.md section 4 cites its measurements.)
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN, int SPEC, int HOPC = 0, bool WIN = false>
 __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     const MfccDev* __restrict__ plan, const TIN* __restrict__ src, int64_t frame_stride,
     int frame_len, int64_t n_frames, float* __restrict__ out, MfccBalance bal) {
@@ -715,18 +655,13 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     // partial tile the waves whose frames all lie past the run skip phase 1
     // (a tile-granular split leaves F / 64 mod G workgroups one full extra
     // tile: a 7-tile makespan for 6.1 tiles of work at 100k frames)
-#ifndef VAD_FRAME_RUNS
-#define VAD_FRAME_RUNS 0  // 1: frame-granular runs (A/B: C2 -1.6 %, C3 +0.7 %)
-#endif
+    // (frame-granular runs measured C2 -1.6 %, C3 +0.7 %: tile runs kept)
     // tile runs balanced over the XCDs' clocks (MfccBalance; word 0: equal)
     const unsigned long long rt0 = bal.stats ? __builtin_amdgcn_s_memrealtime() : 0;
-    const int64_t f_beg = VAD_FRAME_RUNS ? n_frames * blockIdx.x / gridDim.x
-                                         : balanced_tile(bal.word, n_tiles, blockIdx.x, gridDim.x) * kTile;
-    const int64_t f_end0 = VAD_FRAME_RUNS ? n_frames * (blockIdx.x + 1) / gridDim.x
-                                          : balanced_tile(bal.word, n_tiles, blockIdx.x + 1, gridDim.x) * kTile;
+    const int64_t f_beg = balanced_tile(bal.word, n_tiles, blockIdx.x, gridDim.x) * kTile;
+    const int64_t f_end0 = balanced_tile(bal.word, n_tiles, blockIdx.x + 1, gridDim.x) * kTile;
     const int64_t f_end = f_end0 < n_frames ? f_end0 : n_frames;
     auto pair_base = [&](int64_t t, int& lim) {
-      if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
       const int64_t F = f_beg + t * kTile + 2 * grp;
       lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
       return src + (F < flast ? F : flast) * frame_stride;
@@ -740,24 +675,9 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       load_chunks<TIN, 0, NB, LEN>(b0, lim, j, buf);
     }
     __builtin_amdgcn_sched_barrier(0);
-    // DIAG 9: per-workgroup start / end (s_memtime, s_memrealtime) after the
-    // MFCC rows, in a buffer the caller over-allocates; outputs stay exact
-    unsigned long long* wg_st = reinterpret_cast<unsigned long long*>(out + n_frames * 13) + blockIdx.x * 4;
-    (void)wg_st;
-    if constexpr (DIAG == 9 || DIAG == 10) {  // per-workgroup start / end (tools/wgtime.py)
-      if (tid == 0) {
-        wg_st[0] = __builtin_amdgcn_s_memtime();
-        wg_st[1] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
     int64_t prev_f0 = -1;
-    unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
-    (void)stamps;
-    int it = 0;
     // one tile; its buffer is refilled with the next tile's chunks as it frees up
     auto tile_body = [&](v2f (&buf)[NB]) {
-      unsigned long long st_[kStamps];
-      (void)st_;
       const int64_t f0 = f_beg + tile * kTile;
       const int64_t fa = f0 + 2 * grp, fb = fa + 1;
       const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
@@ -772,120 +692,52 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       }
       int lim;
       const TIN* nb = pair_base(tile + 1, lim);
-      // VAD_DCT_AT 1: the deferred DCT at the top of the tile (before phase 1)
-      // on its waves, 2: on waves 4..7 after phase 1 (A/B variants)
-      const int dct_wave = VAD_DCT_AT == 2 ? wave - 4 : wave;
-      if constexpr (MODE == kAudioToMfcc && DIAG != 10 && VAD_DCT_AT == 1) {
-        if (prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
-          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
-        __builtin_amdgcn_sched_barrier(0);
-      }
       if (active) {  // phase 1
         v2f u[16], col[32];
-        // diagnostic builds (DIAG 10 only): XP 1 no LDS transposes (col from
-        // u in registers), XP 3 no FFT arithmetic (loads and LDS traffic only)
-        auto xpose = [&]() __attribute__((always_inline)) {
-          if constexpr (DIAG == 10 && (VAD_DIAG_XP == 1 || VAD_DIAG_XP == 4)) {
-#pragma unroll
-            for (int i = 0; i < 32; ++i) {
-              col[i] = u[i & 15];
-              asm volatile("" : "+v"(col[i]));
-            }
-          } else {
-            store_a(u, gscr, j);
-            read_b(L, gscr, col);
-          }
-        };
-        auto sa = [&](auto off) __attribute__((always_inline)) {
-          constexpr int OFF = decltype(off)::value;
-          if constexpr (DIAG == 10 && (VAD_DIAG_XP == 3 || VAD_DIAG_XP == 4)) {
-#pragma unroll
-            for (int n = 0; n < 16; ++n) {
-              u[n] = Samples<TIN>::cvt(buf[(OFF + n) % NB]);
-              asm volatile("" : "+v"(u[n]));
-            }
-          } else {
-            stage_a_at<TIN, NZ, LEN, OFF, NB, WIN>(buf, L, j, u, wv);
-          }
-        };
-        auto fb_ = [&](float* prow) __attribute__((always_inline)) {
-          if constexpr (DIAG == 10 && VAD_DIAG_XP == 4) {
-            if (col[3].x == 1234.5f) prow[L.e0] = col[7].y;  // keep the loads live, no LDS traffic
-          } else if constexpr (DIAG == 10 && VAD_DIAG_XP == 3) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) prow[L.e0 + 16 * i] = col[i].x + col[16 + i].y;
-          } else {
-            finish_b<MODE == kAudioToSpec>(L, col, prow);
-          }
-        };
-        VAD_STAMP(0);
         VAD_MILESTONE(3);
-        sa(std::integral_constant<int, 0>{});
-        VAD_STAMP(1);
+        stage_a_at<TIN, NZ, LEN, 0, NB, WIN>(buf, L, j, u, wv);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
+        load_chunks<TIN, 0, HOPC, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
-        xpose();
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(2);
         VAD_MILESTONE(2);
         // pass 1's stage A covers the latency of pass 0's transpose reads
-        sa(std::integral_constant<int, HOPC>{});
+        stage_a_at<TIN, NZ, LEN, HOPC, NB, WIN>(buf, L, j, u, wv);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
+        load_chunks<TIN, HOPC, NZ, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(3);
         VAD_MILESTONE(1);
-        if (MODE != kAudioToSpec || fa < f_end) fb_(prow_a);
+        if (MODE != kAudioToSpec || fa < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
         __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(DIAG == 10 && VAD_DIAG_XP == 5)) load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
+        load_chunks<TIN, NZ, NB, LEN>(nb, lim, j, buf);
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(4);
         VAD_MILESTONE(0);
-        xpose();  // after pass 0's reads in program order (LDS is in order per wave)
-        VAD_STAMP(5);
-        if (MODE != kAudioToSpec || fb < f_end) fb_(prow_b);
+        store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
+        read_b(L, gscr, col);
+        if (MODE != kAudioToSpec || fb < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
       }
-      if constexpr (MODE == kAudioToMfcc && DIAG != 10) {  // DIAG 10: phase 1 only (timing)
+      if constexpr (MODE == kAudioToMfcc) {
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(6);
-        if (VAD_DCT_AT != 1 && prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
-          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
-        VAD_STAMP(7);
+        if (prev_f0 >= 0 && wave < kDctGroups)
+          phase2b_any<SPEC, true>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
         lds_barrier();  // P complete; log-mel rows consumed
-        VAD_STAMP(8);
         phase2a<SPEC>(plan, P, lm, wave, lane);
-        VAD_STAMP(9);
         lds_barrier();  // log-mel rows complete; P and the FFT scratch free
-        VAD_STAMP(10);
         prev_f0 = f0;
-        if constexpr (DIAG == 5 || DIAG == 6) {
-          if (lane == 0 && it < 8) {
-#pragma unroll
-            for (int k = 0; k < kStamps; ++k)
-              stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 16 + k] = st_[k];
-          }
-        }
       }
-        };
-    for (; tile < t_end; ++tile, ++it) tile_body(buf);
+    };
+    for (; tile < t_end; ++tile) tile_body(buf);
 
     if constexpr (MODE == kAudioToMfcc) {
-      const int dct_wave = VAD_DCT_AT == 2 ? wave - 4 : wave;
-      if (prev_f0 >= 0 && dct_wave >= 0 && dct_wave < kDctGroups)
-        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, dct_wave, lane, prev_f0, f_end, mfcc_n, out);
+      if (prev_f0 >= 0 && wave < kDctGroups)
+        phase2b_any<SPEC, true>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
     }
     // this run's speed for the host's next balance (runs of >= 8 tiles only:
     // shorter ones are mostly launch ramp)
     if (bal.stats && tid == 0 && t_end >= 8)
       bal.stats[blockIdx.x] = ((unsigned long long)t_end << 40) | (__builtin_amdgcn_s_memrealtime() - rt0);
-    if constexpr (DIAG == 9 || DIAG == 10) {  // per-workgroup start / end (tools/wgtime.py)
-      __syncthreads();
-      if (tid == 0) {
-        wg_st[2] = __builtin_amdgcn_s_memtime();
-        wg_st[3] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
   } else {
     v2f* gscr = scr + grp * kGroupScratch;
     LaneConsts L;
@@ -905,7 +757,6 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     v2f bufA[NZ], bufB[NZ];
     const int64_t flast = n_frames - 1;  // out-of-range frames load the last frame (unused)
     auto pass_src = [&](int64_t t, int pass) {
-      if constexpr (DIAG == 7) t = t & 7;  // diagnostic: L2-resident source
       int64_t f = t * kTile + pass * kGroups + grp;
       f = f < flast ? f : flast;
       return src + f * frame_stride;
@@ -925,16 +776,13 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     __builtin_amdgcn_sched_barrier(0);
     load_pass(tile, 1, bufB);
     __builtin_amdgcn_sched_barrier(0);
-    unsigned long long* stamps = reinterpret_cast<unsigned long long*>(out);
-    int it = 0;
-    (void)stamps;
     int64_t prev_f0 = -1;  // tile whose log-mel rows await phase 2b
     // Per tile and wave: two passes of 4 frames.  Each pass's samples are
     // loaded one tile ahead, right after its stage A consumed the previous
     // ones; pass 1's stage A runs while pass 0's transpose reads are in
     // flight.  sched_barriers pin that order (the scheduler would otherwise
     // hoist the loads or sink the reads).
-    for (; tile < t_end; ++tile, ++it) {
+    for (; tile < t_end; ++tile) {
       const int64_t f0 = tile * kTile;
       const int64_t fa = f0 + grp, fb = f0 + kGroups + grp;
       float* prow_a;
@@ -946,13 +794,8 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         prow_a = P + grp * kPStride;
         prow_b = P + (kGroups + grp) * kPStride;
       }
-      unsigned long long st_[kStamps];
-      (void)st_;
-      // DIAG 6: waves 4..7 skip all work but the barriers
-      const bool work = DIAG != 6 || wave < 4;
-      VAD_STAMP(0);
       v2f u[16], col[32];
-      if (work && LEN > 0 && kSplitLoads && DIAG != 5 && DIAG != 6) {
+      if (LEN > 0) {
         // the next tile's sample loads go out in chunks spread over the
         // tile: a wave's 13 back-to-back pair loads (x 8 waves) would fill
         // the texture address queue and hold every wave at its load burst
@@ -982,9 +825,8 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         __builtin_amdgcn_sched_barrier(0);
         load_stage_a<TIN, NZ, VEC2, LEN, 8, NZ>(sb, len, j, bufB);
         __builtin_amdgcn_sched_barrier(0);
-      } else if (work) {
+      } else {
         stage_a<TIN, NZ, LEN, WIN>(bufA, len, L, j, u, wv);
-        VAD_STAMP(1);
         __builtin_amdgcn_sched_barrier(0);
         load_pass(tile + 1, 0, bufA);
         __builtin_amdgcn_sched_barrier(0);
@@ -993,12 +835,10 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         if constexpr (LEN > 0) {
           // overlap: pass 1's stage A covers the latency of pass 0's reads
           __builtin_amdgcn_sched_barrier(0);
-          VAD_STAMP(2);
           stage_a<TIN, NZ, LEN, WIN>(bufB, len, L, j, u, wv);
           __builtin_amdgcn_sched_barrier(0);
           load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
-          VAD_STAMP(3);
           if (MODE != kAudioToSpec || fa < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
         } else {
           // runtime frame length: the sequential order keeps the generic
@@ -1010,40 +850,26 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
           load_pass(tile + 1, 1, bufB);
           __builtin_amdgcn_sched_barrier(0);
         }
-        VAD_STAMP(4);
         store_a(u, gscr, j);  // after pass 0's reads in program order (LDS is in order per wave)
         read_b(L, gscr, col);
-        VAD_STAMP(5);
         if (MODE != kAudioToSpec || fb < n_frames) finish_b<MODE == kAudioToSpec>(L, col, prow_b);
       }
       if constexpr (MODE == kAudioToMfcc) {
         __builtin_amdgcn_sched_barrier(0);
-        VAD_STAMP(6);
         // the previous tile's DCT runs on the waves that finish phase 1
         // first (waves 0..3 are older and win VALU arbitration on their
         // SIMD) while their SIMD partners are still in their FFT
         if (prev_f0 >= 0 && wave < kDctGroups)
-          phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
-        VAD_STAMP(7);
+          phase2b_any<SPEC, true>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
         lds_barrier();  // P complete; log-mel rows consumed
-        VAD_STAMP(8);
-        if (work) phase2a<SPEC>(plan, P, lm, wave, lane);
-        VAD_STAMP(9);
+        phase2a<SPEC>(plan, P, lm, wave, lane);
         lds_barrier();  // log-mel rows complete; P and the FFT scratch free
-        VAD_STAMP(10);
         prev_f0 = f0;
-        if constexpr (DIAG == 5 || DIAG == 6) {
-          if (lane == 0 && it < 8) {
-#pragma unroll
-            for (int k = 0; k < kStamps; ++k)
-              stamps[(((size_t)blockIdx.x * 8 + wave) * 8 + it) * 16 + k] = st_[k];
-          }
-        }
       }
     }
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
-        phase2b_any<SPEC, DIAG != 5 && DIAG != 6 && !VAD_NO_STORE>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
+        phase2b_any<SPEC, true>(plan, lm, dtb, wave, lane, prev_f0, n_frames, mfcc_n, out);
     }
   }
 }
@@ -1077,11 +903,6 @@ __device__ __forceinline__ Ptr launder(Ptr p) {
   asm volatile("" : "+s"(p));
   return p;
 }
-
-#ifndef VAD_FUSED_DIAG
-#define VAD_FUSED_DIAG 0  // diagnostic builds only: 1 zero weight fragments (no loads), 2 no FFN,
-                          // 5 no FFN and the twiddles kept in VGPRs
-#endif
 
 constexpr int kRingRows = kTile + 4;
 constexpr int kRingFloats = kRingRows * 13;
@@ -1174,12 +995,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
   // requested by the caller before the next tile's last sample batch, so the
   // vmcnt wait for them does not also wait for those samples.
   auto fetch_frags = [&](u4 (&frh)[HP::NS][2]) __attribute__((always_inline)) {
-    if constexpr (VAD_FUSED_DIAG == 1) {
-#pragma unroll
-      for (int sl = 0; sl < HP::NS; ++sl) frh[sl][0] = frh[sl][1] = (u4){0u, 0u, 0u, 0u};
-    } else {
-      load_fragh<HP>(reinterpret_cast<const uint32_t*>(launder(net.fragh)), lane, frh);
-    }
+    load_fragh<HP>(reinterpret_cast<const uint32_t*>(launder(net.fragh)), lane, frh);
   };
   auto ffn_tile = [&](int tt, u4 (&frh)[HP::NS][2]) __attribute__((always_inline)) {
     const float* R = ring + (tt & 1) * kRingFloats + 16 * wave * MN;
@@ -1204,7 +1020,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
   for (int t = 0; t < n_t; ++t) {
     // twiddles from LDS each tile: dead (and their VGPRs free for the FFN)
     // between phase 1 and the next tile
-    if (VAD_FUSED_DIAG != 5 || t == 0) lane_consts_lds(tw, j, L);
+    lane_consts_lds(tw, j, L);
     float* prow_a = P + (2 * grp) * kPStride;
     float* prow_b = P + (2 * grp + 1) * kPStride;
     int lim;
@@ -1234,7 +1050,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     finish_b<false>(L, col, prow_b);
     __builtin_amdgcn_sched_barrier(0);
     if (wave < kDctGroups) {
-      if (VAD_FUSED_DIAG != 2 && t >= 2) {
+      if (t >= 2) {
         u4 frh[HP::NS][2];
         fetch_frags(frh);
         __builtin_amdgcn_sched_barrier(0);
@@ -1251,14 +1067,14 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     phase2a<SPEC>(plan, P, lm, wave, lane);
     lds_barrier();  // log-mel rows complete; P and the FFT scratch free
   }
-  if (VAD_FUSED_DIAG != 2 && wave < kDctGroups) {
+  if (wave < kDctGroups) {
     u4 frh[HP::NS][2];
     fetch_frags(frh);
     dct_to_ring(n_t - 1);
     if (n_t >= 2) ffn_tile(n_t - 2, frh);
   }
   lds_barrier();
-  if (VAD_FUSED_DIAG != 2 && wave < kDctGroups) {
+  if (wave < kDctGroups) {
     u4 frh[HP::NS][2];
     fetch_frags(frh);
     ffn_tile(n_t - 1, frh);
@@ -1277,20 +1093,11 @@ static int num_cus() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
       n = 256;
-#if VAD_DIAG_BUILD != 0
-    // diagnostic libraries only: VAD_MFCC_CUS=n runs the persistent grid on
-    // fewer workgroups (clock-versus-load experiments, tools/wgtime.py)
-    if (const char* e = getenv("VAD_MFCC_CUS")) {
-      const int k = atoi(e);
-      if (k > 0 && k < n) n = k;
-    }
-#endif
   }
   return n;
 }
 
-template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int DIAG = 0,
-          int HOPC = 0, bool WIN = false>
+template <typename TIN, int MODE, int NZ, bool VEC2, int LEN = 0, int SPEC = 0, int HOPC = 0, bool WIN = false>
 static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, int len,
                            int64_t n, float* out, hipStream_t st, const MfccBalance& bal = MfccBalance()) {
   const int64_t n_tiles = (n + kTile - 1) / kTile;
@@ -1299,10 +1106,10 @@ static hipError_t launch_t(const MfccDev* plan, const TIN* src, int64_t stride, 
   const size_t smem = mfcc_smem_bytes();
   static std::atomic<unsigned long long> attr_done{0};
   const hipError_t e = ensure_dyn_lds(
-      reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC, WIN>), (int)smem,
+      reinterpret_cast<const void*>(&mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, HOPC, WIN>), (int)smem,
       attr_done);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, DIAG, HOPC, WIN>), dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL((mfcc_kernel<TIN, MODE, NZ, VEC2, LEN, SPEC, HOPC, WIN>), dim3(grid), dim3(kThreads),
                      smem, st, plan, src, stride, len, n, out, bal);
   return hipGetLastError();
 }
@@ -1314,42 +1121,35 @@ static hipError_t launch_m(const MfccDev* plan, int spec, const TIN* src, int64_
   const bool vec2 = ((reinterpret_cast<uintptr_t>(src) % Samples<TIN>::kPairAlign) == 0) &&
                     ((stride & 1) == 0) && ((used & 1) == 0);
   if ((spec == kSpecWindow || spec == kSpecWindow26 || spec == kSpecWindow40) && used == 400 && vec2 &&
-      stride == 160 && kPairFrames) {
+      stride == 160) {
     // optional analysis window at the reference framing: the paired-frame
     // kernel with the window applied in its stage A (and the generated mel
     // code when the bank is a compiled one)
-    if (spec == kSpecWindow26) return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
-    if (spec == kSpecWindow40) return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
-    return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
+    if (spec == kSpecWindow26) return launch_t<TIN, MODE, 13, true, 400, 1, 5, true>(plan, src, stride, len, n, out, st, bal);
+    if (spec == kSpecWindow40) return launch_t<TIN, MODE, 13, true, 400, 2, 5, true>(plan, src, stride, len, n, out, st, bal);
+    return launch_t<TIN, MODE, 13, true, 400, 0, 5, true>(plan, src, stride, len, n, out, st, bal);
   }
   if (spec == kSpecWindow26 || spec == kSpecWindow40) spec = kSpecWindow;
   if (spec == kSpecWindow) {  // optional analysis window: the runtime-table kernel with WIN
     if (used <= 32 * 13)
-      return vec2 ? launch_t<TIN, MODE, 13, true, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
-                  : launch_t<TIN, MODE, 13, false, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
-    return vec2 ? launch_t<TIN, MODE, 16, true, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
-                : launch_t<TIN, MODE, 16, false, 0, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
+      return vec2 ? launch_t<TIN, MODE, 13, true, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
+                  : launch_t<TIN, MODE, 13, false, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
+    return vec2 ? launch_t<TIN, MODE, 16, true, 0, 0, 0, true>(plan, src, stride, len, n, out, st)
+                : launch_t<TIN, MODE, 16, false, 0, 0, 0, true>(plan, src, stride, len, n, out, st);
   }
   if (used == 400 && vec2) {  // the reference framing (config.py:21): fully specialised
     if (MODE == kAudioToMfcc && spec == 1) {
-      if constexpr (VAD_DIAG_BUILD != 0) {  // diagnostic library builds only (outputs wrong)
-        constexpr int D = VAD_DIAG_BUILD == 8 ? 5 : VAD_DIAG_BUILD;
-        constexpr bool kPairedDiag = D == 5 || D == 7 || D == 9 || D == 10;
-        if (kPairedDiag && VAD_DIAG_BUILD != 8 && stride == 160 && kPairFrames)
-          return launch_t<TIN, MODE, 13, true, 400, 1, D, 5>(plan, src, stride, len, n, out, st);
-        return launch_t<TIN, MODE, 13, true, 400, 1, D == 9 || D == 10 ? 0 : D>(plan, src, stride, len, n, out, st);
-      }
-      if (stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 1, 0, 5>(plan, src, stride, len, n, out, st, bal);
+      if (stride == 160)
+        return launch_t<TIN, MODE, 13, true, 400, 1, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 1>(plan, src, stride, len, n, out, st);
     }
     if (MODE == kAudioToMfcc && spec == 2) {
-      if (stride == 160 && kPairFrames)
-        return launch_t<TIN, MODE, 13, true, 400, 2, 0, 5>(plan, src, stride, len, n, out, st, bal);
+      if (stride == 160)
+        return launch_t<TIN, MODE, 13, true, 400, 2, 5>(plan, src, stride, len, n, out, st, bal);
       return launch_t<TIN, MODE, 13, true, 400, 2>(plan, src, stride, len, n, out, st);
     }
-    if (stride == 160 && kPairFrames)
-      return launch_t<TIN, MODE, 13, true, 400, 0, 0, 5>(plan, src, stride, len, n, out, st, bal);
+    if (stride == 160)
+      return launch_t<TIN, MODE, 13, true, 400, 0, 5>(plan, src, stride, len, n, out, st, bal);
     return launch_t<TIN, MODE, 13, true, 400>(plan, src, stride, len, n, out, st);
   }
   if (used <= 32 * 13) {
@@ -1392,7 +1192,7 @@ hipError_t launch_mfcc_i16(int mode, const MfccDev* plan, int spec, const int16_
 // compiled 26-filter bank and a split-f16 topology; false -> the caller runs
 // the two-kernel path through a workspace.
 bool mfcc_ffn_fusable(int spec, const FfnDev& net, int frame_size, int hop, const void* audio, int tin_bytes) {
-  if (!kPairFrames || spec != 1 || frame_size != 400 || hop != 160 || !net.fragh) return false;
+  if (spec != 1 || frame_size != 400 || hop != 160 || !net.fragh) return false;
   if (reinterpret_cast<uintptr_t>(audio) % (2 * tin_bytes) != 0) return false;  // sample-pair loads
   const int* t = net.tiles;
   const bool ref39 = net.n_layers == 4 && net.ks0 == 10 && t[0] == 4 && t[1] == 2 && t[2] == 1 && t[3] == 1;

@@ -140,9 +140,6 @@ hipError_t launch_preemphasis(const float* x, float* y, int64_t n_rows, int64_t 
 // Per-wave LDS scratch (floats): the FFT's ping-pong buffers (the power
 // row reuses the first once the transform is done), the log-mel row, two
 // activation rows.
-#ifndef VAD_HOP_DIAG
-#define VAD_HOP_DIAG 0  // diagnostic builds only: stop after 1 staging, 2 FFT, 3 mel / DCT, 4 features
-#endif
 #ifndef VAD_HOP_Q
 #define VAD_HOP_Q 4
 #endif
@@ -290,10 +287,6 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       }
     }
     uint8_t* lab_k = labels + (int64_t)k * lab_kstride;
-    if (VAD_HOP_DIAG == 1) {
-      if (ln == 0) lab_k[s] = (uint8_t)v[0];
-      continue;
-    }
     // samples of the FFT (np.fft.fft(x, 512): zero-pad / truncate, mfcc.py:61)
     float* xs = reinterpret_cast<float*>(z1);
 #pragma unroll
@@ -332,10 +325,6 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       dst = t;
       asm volatile("" ::: "memory");
     }
-    if (VAD_HOP_DIAG == 2) {
-      if (ln == 0) lab_k[s] = (uint8_t)src[3].x;
-      continue;
-    }
     // -- real-FFT split: 2X[k] = S - i W512^k D, S = Z[k] + conj(Z[-k]),
     // D = Z[k] - conj(Z[-k]); |2X|^2 into the free buffer
     float* pw = reinterpret_cast<float*>(dst);
@@ -371,11 +360,6 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
 #pragma unroll 8
       for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
     }
-
-    if (VAD_HOP_DIAG == 3) {
-      if (ln == 0) lab_k[s] = (uint8_t)mf;
-      continue;
-    }
     // -- window of the five previous frames, then push the new row
     const bool have = c >= 5;
     act_a[ln] = 0.f;  // feature columns past 3 mfcc_n: zero (the FFN reads them in fours)
@@ -409,7 +393,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     }
     asm volatile("" ::: "memory");
     uint8_t label = 255;
-    if (have && VAD_HOP_DIAG != 4) {
+    if (have) {
       // -- FFN: exact f32, ln o of each layer
       float* hin = act_a;
       float* hout = act_b;
