@@ -25,7 +25,7 @@ LABEL_MARGIN = 0.05
 SPLIT_VS_F32 = 2.5  # measured 1.05x (13-64-64-2) and 1.5x (39-64-32-16-3)
 # windows of the C3 clip whose label differs from the fp64 oracle (all of them
 # below LABEL_MARGIN; the count and margins are reported by label_agreement)
-C3_MAX_DISAGREE = 20
+C3_MAX_DISAGREE = 2  # observed (profiles/r04/label_agreement_c3.json): 2 windows, margins 3.2e-6 / 3.7e-6
 
 
 @pytest.fixture(scope="module")
@@ -133,6 +133,8 @@ def test_c3_full_clip_vs_oracle(torch_cuda):
                                  "below_label_margin": int((~sure).sum()), "label_margin": LABEL_MARGIN})
     np.testing.assert_array_equal(got[sure], ref_l[sure])
     assert rep["disagree"] <= C3_MAX_DISAGREE, rep["disagree_windows"]
+    # the ones there are sit at the fp32-vs-fp64 MFCC rounding scale
+    assert all(d["margin"] < 1e-5 for d in rep["disagree_windows"]), rep["disagree_windows"]
     # and exactly the oracle's FFN on the device's own features where the
     # margin clears the forward's rounding
     xg = window_features(m).cpu().numpy()[:, :13]
