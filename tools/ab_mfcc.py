@@ -32,7 +32,12 @@ k = [0]
 def c2f():
     pipe.mfcc(cl[k[0] % 6], out=m); k[0] += 1
 c2 = t(c2f)
-print(json.dumps({"c3_us": c3, "c2_us": c2}))
+from vad_amd.config import MfccConfig
+p40 = VadPipeline(cfg=MfccConfig(n_filters=40))
+def c2g():
+    p40.mfcc(cl[k[0] % 6], out=m); k[0] += 1
+c2_40 = t(c2g)
+print(json.dumps({"c3_us": c3, "c2_us": c2, "c2_40_us": c2_40}))
 '''
 
 args = sys.argv[1:]
