@@ -515,9 +515,11 @@ def main():
     # between two kernels idles the GPU for ~5 us, so the timed steps carry
     # none)
     # (batches of 10 launches between event pairs: the mean over all of them,
-    # and p10 / p50 / p90 of the batch means)
+    # and p10 / p50 / p90 of the batch means; at least 30 batches, so that one
+    # slow batch -- a clock dip, a neighbour's burst on the node -- moves the
+    # mean by a thirtieth of its excess rather than a tenth)
     def kernel_ms(fn, batch=10):
-        nb = max(1, args.steps // batch)
+        nb = max(30, args.steps // batch)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(nb + 1)]
         ev[0].record(stream)
         for i in range(nb):
