@@ -191,3 +191,47 @@ def test_tree_oracle_matches_live_sklearn():
     Xt = np.round(rng.standard_normal((2000, 7)) * 4).astype(np.float32) / 4
     Xt[rng.random(Xt.shape) < 0.05] = np.nan
     assert np.array_equal(O.tree_predict(O.tree_arrays(clf), Xt), clf.predict(Xt))
+
+
+def _sklearn_mlp(layers, n_classes):
+    """scikit-learn's MLPClassifier carrying `layers` (Keras (in, out) layout,
+    relu hidden layers): an independent implementation of the forward the
+    oracle restates (ffn_trainer.py:106-116).  Two classes: sklearn's binary
+    output is one logistic unit, i.e. the softmax of (z0, z1) folded into
+    z1 - z0."""
+    import warnings
+    from sklearn.exceptions import ConvergenceWarning
+    from sklearn.neural_network import MLPClassifier
+    hidden = tuple(w.shape[1] for w, _ in layers[:-1])
+    clf = MLPClassifier(hidden_layer_sizes=hidden, activation="relu", max_iter=1, random_state=0)
+    rng = np.random.default_rng(0)
+    xs = rng.standard_normal((4 * n_classes, layers[0][0].shape[0]))
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", ConvergenceWarning)
+        clf.fit(xs, np.arange(4 * n_classes) % n_classes)
+    ws = [np.asarray(w, np.float64) for w, _ in layers]
+    bs = [np.asarray(b, np.float64) for _, b in layers]
+    if n_classes == 2:
+        ws[-1] = (ws[-1][:, 1] - ws[-1][:, 0])[:, None]
+        bs[-1] = np.array([bs[-1][1] - bs[-1][0]])
+    clf.coefs_, clf.intercepts_ = ws, bs
+    return clf
+
+
+@pytest.mark.parametrize("topo,n_classes", [("ref39", 3), ("bl13", 2)])
+def test_ffn_oracle_matches_sklearn_mlp(golden, topo, n_classes):
+    """The fp64 FFN restatement (Keras is absent) against live
+    scikit-learn's MLP forward on the fixture weights and feature rows:
+    probabilities to 1e-12 and labels exactly (finite rows: sklearn rejects
+    NaN input; the NaN rule is test_nan_label_is_zero's)."""
+    g = golden("ffn")
+    n = 4 if topo == "ref39" else 3
+    layers = [(g[f"{topo}_W{i}"], g[f"{topo}_b{i}"]) for i in range(n)]
+    x = g["test_x"] if topo == "ref39" else g["test_x"][:, :13]
+    x = x[np.isfinite(x).all(axis=1)]
+    assert len(x) > 500
+    clf = _sklearn_mlp(layers, n_classes)
+    _, p = O.ffn_forward(x, layers)
+    sp = clf.predict_proba(x)
+    np.testing.assert_allclose(sp, p, rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(clf.predict(x), O.ffn_labels(x, layers))
