@@ -202,7 +202,10 @@ class StreamBatch:
         """One step (K hops) from ``host_inputs`` to ``host_labels``: H2D
         copy, the hop kernel(s), D2H copy, all on the current stream (the
         caller synchronises it before reading host_labels).  Replays the
-        graph when capture(host_io=True) recorded one."""
+        graph when capture(host_io=True) recorded one.  The copies are
+        asynchronous: a producer rewrites host_inputs only once the stream
+        has passed the previous step's H2D copy (a stream or event sync, as
+        vad.py's loop would do before reading the labels anyway)."""
         if self.host_inputs is None:
             raise ValueError("attach_host_io() (or capture(host_io=True)) first")
         if self.graph is not None and self.graph_host_io:
