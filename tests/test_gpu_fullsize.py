@@ -271,3 +271,41 @@ def test_clip_past_2g_samples(torch_cuda):
         assert torch.equal(pipe.labels(cut), big_lab[f0:f0 + W - 5]), f0
     del audio, big, big_lab
     torch.cuda.empty_cache()
+
+
+def test_kernel_time_guard(torch_cuda):
+    """A regression guard on the benchmark kernels (C3 sizes, 1M frames):
+    the MFCC kernel under 0.30 ms and the 13-64-64-2 FFN kernel under
+    0.08 ms per launch (mean of 100 launches after a 0.3 s warm-up; measured
+    0.24-0.26 / 0.051-0.056 ms across round-4 boxes), so
+    a change that loses 20 % on either fails here, not only in the bench."""
+    import time
+    torch = torch_cuda
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 1_000_000
+    clip = O.synth_clip(O.samples_for_frames(F), seed=1)
+    pipe = VadPipeline(FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)))
+    a = torch.from_numpy(clip).cuda()
+    m = torch.empty((F, 13), dtype=torch.float32, device="cuda")
+    lab = torch.empty((F - 5,), dtype=torch.uint8, device="cuda")
+    plan = pipe.ffn.plan
+
+    def mean_ms(fn, reps=100):
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.3:
+            fn()
+            torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
+
+    t_mfcc = mean_ms(lambda: pipe.mfcc(a, out=m))
+    t_ffn = mean_ms(lambda: plan.window_labels(m, out=lab))
+    print(f"kernel time guard: MFCC {t_mfcc * 1e3:.1f} us, FFN {t_ffn * 1e3:.1f} us per 1M frames")
+    assert t_mfcc < 0.30, t_mfcc
+    assert t_ffn < 0.08, t_ffn
