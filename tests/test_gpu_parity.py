@@ -511,6 +511,50 @@ def test_stream_hop_blocks_equal_single_hops(torch_cuda, golden, kernel, K):
     assert (want[:5] == 255).all() and (want[5:] != 255).all()
 
 
+def test_stream_hop_block_stream_major(torch_cuda, golden):
+    """A block in stream-major order -- each stream's K hops contiguous, an
+    (S, K * hop) buffer viewed as (K, S, hop): block stride hop, row stride
+    K * hop -- is read in place by vad_stream_hops (disjoint rows, the other
+    ordering) and gives the labels and state of K single-hop steps; a view
+    whose rows overlap falls back to a copy in step_block."""
+    import torch
+    from vad_amd import _lib
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch, hop_rows_disjoint
+    w = golden("ffn")
+    clf = FFNClassifier(layers_from(w, "ref39", 4))
+    S, K, nb = 24, 8, 3
+    T = K * nb
+    clips = [O.synth_clip(160 * (T - 1) + 401, seed=850 + s) for s in range(S)]
+    carry = torch.from_numpy(np.stack([c[:240] for c in clips])).cuda()
+    per_stream = torch.from_numpy(np.stack([c[240:240 + 160 * T] for c in clips])).cuda()  # (S, T*hop)
+    ref = StreamBatch(S, clf)
+    ref.prime(carry)
+    want = torch.stack([ref.step(per_stream[:, 160 * t:160 * (t + 1)].contiguous()).clone() for t in range(T)])
+    sb = StreamBatch(S, clf, hops_per_step=K)
+    sb.prime(carry)
+    got = []
+    for b in range(nb):
+        blk = per_stream[:, 160 * K * b:160 * K * (b + 1)].contiguous().view(S, K, 160).transpose(0, 1)
+        assert blk.stride() == (160, K * 160, 1) and hop_rows_disjoint(S, K, 160, K * 160, 160)
+        got.append(sb.step_block(blk).clone())
+    got = torch.cat(got)
+    assert torch.equal(got, want), int((got != want).sum())
+    assert torch.equal(sb.frames, ref.frames) and torch.equal(sb.ring, ref.ring)
+    # the C ABI itself accepts that layout (rc 0) and refuses an overlapping one
+    L = _lib.lib()
+    ok = per_stream[:, :160 * K].contiguous()
+    rc = L.vad_stream_hops(sb.plan.handle, sb.ffn.plan.handle, _lib.ptr(sb.frames), 400, 400, _lib.ptr(ok),
+                           K * 160, 160, S, K, 160, _lib.ptr(sb.ring), _lib.ptr(sb.count),
+                           _lib.ptr(sb.label_block), S, _lib.stream_ptr())
+    assert rc == 0
+    rc = L.vad_stream_hops(sb.plan.handle, sb.ffn.plan.handle, _lib.ptr(sb.frames), 400, 400, _lib.ptr(ok),
+                           K * 160 - 1, 160, S, K, 160, _lib.ptr(sb.ring), _lib.ptr(sb.count),
+                           _lib.ptr(sb.label_block), S, _lib.stream_ptr())
+    assert rc == _lib.VAD_EINVAL
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("K,graph", [(1, False), (1, True), (8, False), (8, True)])
 def test_stream_host_io_steps(torch_cuda, golden, K, graph):
     """C5 as SURVEY 8(d) times it: each step copies every stream's new

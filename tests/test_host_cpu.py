@@ -209,3 +209,18 @@ def test_bench_refuses_world_size_mismatch():
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert "disagrees with WORLD_SIZE" in r.stderr
+
+
+def test_hop_rows_disjoint_layouts():
+    """The in-place hop-block layouts (stream.py hop_rows_disjoint, the same
+    rule as capi.hip vad_hop_layout_disjoint): hop-major and stream-major
+    blocks pass, repeating / overlapping / backwards blocks do not."""
+    from vad_amd.stream import hop_rows_disjoint
+    S, K, H = 24, 8, 160
+    assert hop_rows_disjoint(S, K, S * H, H, H)            # (K, S, hop) contiguous
+    assert hop_rows_disjoint(S, K, H, K * H, H)            # (S, K*hop) viewed as (K, S, hop)
+    assert hop_rows_disjoint(S, 1, 0, H, H)                # one hop: nothing to overlap
+    assert not hop_rows_disjoint(S, K, 0, H, H)            # the same block K times
+    assert not hop_rows_disjoint(S, K, -S * H, H, H)       # backwards
+    assert not hop_rows_disjoint(S, K, 3 * H, H, H)        # blocks overlap
+    assert not hop_rows_disjoint(S, K, H, K * H - 1, H)    # stream rows overlap

@@ -150,6 +150,16 @@ struct vad_mfcc_plan {
 // The spec a launch passes: a windowed plan whose bank is a compiled one
 // says which (kSpecWindow26 / 40), so the reference framing keeps the
 // generated mel code; vad_mfcc_plan_variant still reports kSpecWindow.
+// n_hops > 1 blocks of n_streams hop rows: disjoint in either ordering
+// (hop-major: each block past the previous block's last row; stream-major:
+// each row's K hops before the next row), never repeating (block stride > 0)
+static bool vad_hop_layout_disjoint(int64_t n_streams, int32_t n_hops, int64_t block_stride, int64_t hop_stride,
+                                    int32_t hop_len) {
+  if (block_stride <= 0) return false;
+  if (block_stride >= (n_streams - 1) * hop_stride + hop_len) return true;
+  return hop_stride >= (int64_t)(n_hops - 1) * block_stride + hop_len;
+}
+
 static int launch_spec(const vad_mfcc_plan* p) {
   if (p->spec != kSpecWindow) return p->spec;
   return p->table_spec == 1 ? kSpecWindow26 : p->table_spec == 2 ? kSpecWindow40 : kSpecWindow;
@@ -830,9 +840,13 @@ int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* f
       hop_len > frame_len || frame_stride < frame_len || hop_stride < hop_len)
     return VAD_EINVAL;
   if (n_hops > 1 && label_block_stride < n_streams) return VAD_EINVAL;  // label rows of two hops would overlap
-  // hop k's block must not be hop k-1's: a zero or negative stride would
-  // replay (or walk backwards over) the new samples
-  if (n_hops > 1 && hop_block_stride < (n_streams - 1) * hop_stride + hop_len) return VAD_EINVAL;
+  // hop k's block must not be hop k-1's (a zero or negative stride would
+  // replay, or walk backwards over, the new samples), and no two (hop,
+  // stream) rows may overlap: either ordering of a disjoint layout is fine,
+  // hop-major (blocks of S rows) or stream-major ((S, K*hop) viewed as
+  // (K, S, hop): block stride hop, row stride K*hop)
+  if (n_hops > 1 && !vad_hop_layout_disjoint(n_streams, n_hops, hop_block_stride, hop_stride, hop_len))
+    return VAD_EINVAL;
   if (n_streams == 0 || n_hops == 0) return VAD_OK;
   if (!frames || !hop || !ring || !count || !labels) return VAD_EINVAL;
   if (ffn->net.dims[0] > 3 * plan->host.mfcc_n) return VAD_EINVAL;

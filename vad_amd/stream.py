@@ -44,6 +44,19 @@ from .ffn import FFNClassifier
 from .plan import MfccPlan
 
 
+def hop_rows_disjoint(n_streams, n_hops, block_stride, hop_stride, hop_len):
+    """The layouts vad_stream_hops reads in place (capi.hip
+    vad_hop_layout_disjoint): one hop only, or hop rows that neither repeat
+    nor overlap, in hop-major order ((K, S, hop) blocks) or stream-major
+    order (an (S, K * hop) buffer viewed as (K, S, hop))."""
+    if n_hops <= 1:
+        return True
+    if block_stride <= 0:
+        return False
+    return (block_stride >= (n_streams - 1) * hop_stride + hop_len
+            or hop_stride >= (n_hops - 1) * block_stride + hop_len)
+
+
 class StreamBatch:
 
     def __init__(self, n_streams, ffn, cfg: MfccConfig = MfccConfig(), device=None, kernel="hop",
@@ -167,7 +180,8 @@ class StreamBatch:
             if new_samples.shape != self.inputs.shape or new_samples.dtype != torch.float32 \
                     or not new_samples.is_cuda:
                 raise ValueError(f"new_samples must be a CUDA float32 tensor of shape {tuple(self.inputs.shape)}")
-            if (self.graph is None or self.graph_host_io) and self.kernel == "hop" and new_samples.stride(2) == 1:
+            if (self.graph is None or self.graph_host_io) and self.kernel == "hop" and new_samples.stride(2) == 1 \
+                    and hop_rows_disjoint(self.n, self.K, new_samples.stride(0), new_samples.stride(1), self.cfg.hop):
                 self._hop_call(new_samples, self.K, self.label_block)  # read in place
                 return self.label_block
             self.inputs.copy_(new_samples)
