@@ -181,6 +181,39 @@ __device__ __forceinline__ f32x4 valu_out_layer(FV fv, const f32x4 (&h)[TI], flo
   return z;
 }
 
+// Two-class label from the logit difference (labels-only launches of a
+// network whose output layer runs on the VALU, 13-64-64-2): z1 - z0 =
+// (W1 - W0) h + (b1 - b0) as ONE dot product per lane -- fd holds the TI*4
+// difference weights of the lane group, then the bias difference (staged by
+// the kernel, f32 differences of the plan's slots) -- instead of one per
+// class, so label = d > 0 wherever the logits are finite: np.argmax's
+// choice whenever the two logits differ by more than their rounding (a
+// near-tie may fall either way, as between any two f32 summation orders; the
+// labels' parity is the fp64 oracle's margin rule).  A
+// non-finite d in a window that is not flagged (an overflowed layer) reruns
+// the wave's output layer in the two-logit form, whose argmax rules (NaN,
+// +-inf) decide then; a flagged window (wnan: its logits are NaN) is class 0.
+template <class TP, int TI, class FD, class FV>
+__device__ __forceinline__ int valu_label2(FD fd, FV fv, const f32x4 (&h)[TI], int wnan) {
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int t = 0; t < TI; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; r += 2) {
+      p0 = fmaf(fd[t * 4 + r], h[t][r], p0);
+      p1 = fmaf(fd[t * 4 + r + 1], h[t][r + 1], p1);
+    }
+  }
+  const float d = lane_sum_xor48(p0 + p1) + fd[TI * 4];
+  const bool bad = !wnan && !(__builtin_fabsf(d) < INFINITY);
+  if (__builtin_amdgcn_ballot_w64(bad)) {  // wave-uniform and rare: the two-logit rules
+    f32x4 z = valu_out_layer<TP, TI, FV>(fv, h);
+    if (wnan) z = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    return argmax_classes(z, 2);
+  }
+  return wnan ? 0 : (d > 0.f);
+}
+
 template <int KS0, int T1, int T2, int T3, int T4, int NC>
 __device__ __forceinline__ f32x4 mlp_forward(const float* __restrict__ fa, const float* __restrict__ fb,
                                              const float* __restrict__ fv, const float (&x)[KS0]) {
@@ -511,6 +544,21 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)
 }
 
 
+// The hidden layers of a three-layer split-f16 network whose output layer
+// runs on the VALU (13-64-64-2): the last hidden layer's accumulator tiles,
+// for valu_label2.
+template <int KS0, int T1, int T2, class FB, bool IN_BOUNDED, class FH>
+__device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS0 + 31) / 32][8], f32x4 (&h2)[T2]) {
+  using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
+  using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
+  static_assert(TP::NL == 3 && TP::VL, "three layers, the output layer on the VALU");
+  f32x4 h1[T1];
+  dense_h3<T1, HP::K0, FB, false, kMerge0<KS0>, IN_BOUNDED>(fh, fb, x0, h1, true);
+  float v1[HP::K1][8];
+  acts_of<T1>(h1, v1);
+  dense_h3<T2, HP::K1, FB, true>(fh.at(HP::S0), fb + 4 * T1, v1, h2, true);
+}
+
 // Per-lane fragment slots read straight from global memory (L1 / L2
 // resident: the plan's tables are a few tens of KB), for kernels whose VGPRs
 // and LDS are taken by other work (the fused MFCC + FFN kernel).
@@ -596,7 +644,7 @@ __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, 
 // Layer-0 B operands of window lane & 15 from X (lane (g, jw) holds
 // features 32 s + 8 g + q of window jw) and the window's NaN flag.  MASK:
 // X's columns IN .. 32 K0 - 1 hold stale data (not kept zero) and are zeroed
-// in registers.
+// in registers; without it the caller keeps them zero.
 template <int K0, int IN, int XS, bool MASK>
 __device__ __forceinline__ int wave_tile_operands(const float* __restrict__ X, const int* __restrict__ FL,
                                                   int lane, float (&x0)[K0][8]) {
@@ -610,9 +658,11 @@ __device__ __forceinline__ int wave_tile_operands(const float* __restrict__ X, c
       x0[0][q] = lo4[q];
       x0[0][q + 4] = hi4[q];
     }
+    if constexpr (MASK) {  // else X's columns IN .. 15 are kept zero by the caller
 #pragma unroll
-    for (int q = 0; q < 8; ++q)
-      if (8 + q >= IN) x0[0][q] = 8 * (g & 1) + q < IN ? x0[0][q] : 0.f;
+      for (int q = 0; q < 8; ++q)
+        if (8 + q >= IN) x0[0][q] = 8 * (g & 1) + q < IN ? x0[0][q] : 0.f;
+    }
     return FL[jw];
   }
   const v4f* xr = reinterpret_cast<const v4f*>(X + jw * XS + 8 * g);
@@ -663,6 +713,21 @@ __device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, c
   float x0[K0][8];
   const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
   return wave_tile_mlp<KS0, T1, T2, T3, T4, NC, NOVL, IN_BOUNDED>(x0, wnan, fh, fb, fv, n_classes, z);
+}
+
+// Label of window lane & 15 by the logit difference (valu_label2): the
+// labels-only launches of a 13-64-64-2-shaped network; fd = the lane group's
+// difference slots (TI*4 weights, then the bias).
+template <int KS0, int T1, int T2, int IN, int XS, bool MASK, bool IN_BOUNDED, class FH, class FB, class FV, class FD>
+__device__ __forceinline__ int wave_tile_label2(const float* __restrict__ X, const int* __restrict__ FL, int lane,
+                                                FH fh, FB fb, FV fv, FD fd) {
+  constexpr int K0 = (4 * KS0 + 31) / 32;
+  using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
+  float x0[K0][8];
+  const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
+  f32x4 h2[T2];
+  mlp_hidden2_h3<KS0, T1, T2, FB, IN_BOUNDED>(fh, fb, x0, h2);
+  return valu_label2<TP, T2>(fd, fv, h2, wnan);
 }
 
 // optional logits output (FfnDev::logits, tests): row w's fp32 logits

@@ -372,7 +372,10 @@ constexpr int kWRowRegs = (kWRows + 63) / 64;    // 5 per lane
 #define VAD_FFN_WPB 4  // waves per block (sharing one LDS fragment copy)
 #endif
 constexpr int kWpb = VAD_FFN_WPB;
-template <int KS0, int T1, int T2, int T3, int T4, int NC, int MODE>
+// LG: the launch also writes the logits (net.logits, tests); without it a
+// two-class network with a VALU output layer (13-64-64-2) takes its labels
+// from the logit difference (valu_label2: one dot product instead of two)
+template <int KS0, int T1, int T2, int T3, int T4, int NC, int MODE, bool LG>
 __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveResidency<KS0, NC>::kWavesPerSimd))) void ffn_wave_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
   // VAD_FFN_WAVE_MFMA_OUT: the output layer on the MFMA too (the plan's
@@ -398,7 +401,10 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   constexpr bool kLdsFrags = WaveResidency<KS0, NC>::kLdsFrags;
   constexpr bool kLdsSlots = WaveResidency<KS0, NC>::kLdsSlots;
   constexpr int NSL = TP::NB + TP::NV + TP::NVB;  // bias + output-layer slots
-  constexpr int NSLP = (NSL + 3) & ~3;
+  // the logit-difference slots (valu_label2): TIL*4 weights, then the bias
+  constexpr bool kDiff = !LG && NC == 2 && TP::VL && TP::NL == 3 && kLdsSlots;
+  constexpr int NSD = kDiff ? TP::TIL * 4 + 1 : 0;
+  constexpr int NSLP = (NSL + NSD + 3) & ~3;
   __shared__ __attribute__((aligned(16))) float slot_s[kLdsSlots ? 4 * NSLP : 1];
 #ifndef VAD_FFN_LO_ALL
 #define VAD_FFN_LO_ALL 1  // 1: every lo half in LDS; 0: those after layer 0 only
@@ -412,12 +418,23 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   if constexpr (kLdsSlots) {
     // slot sl of lane group gg (the host's fragment order: biases, then the
     // VALU layer's class slots, then its biases after 4 classes' worth)
-    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kWpb) {
-      const int gg = i / NSLP, sl = i - gg * NSLP;
+    auto slot_val = [&](int sl, int gg) {
       const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
                                      : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
                                                                                   : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
-      slot_s[i] = sl < NSL ? net.frag[src_sl * 64 + 16 * gg] : 0.f;
+      return net.frag[src_sl * 64 + 16 * gg];
+    };
+    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kWpb) {
+      const int gg = i / NSLP, sl = i - gg * NSLP;
+      float v = 0.f;
+      if (sl < NSL) {
+        v = slot_val(sl, gg);
+      } else if (sl < NSL + NSD) {  // class 1 minus class 0 (weights, then the bias)
+        const int q = sl - NSL;
+        v = q < TP::TIL * 4 ? slot_val(TP::NB + TP::TIL * 4 + q, gg) - slot_val(TP::NB + q, gg)
+                            : slot_val(TP::NB + TP::NV + 1, gg) - slot_val(TP::NB + TP::NV, gg);
+      }
+      slot_s[i] = v;
     }
     // the lo halves of the layers after the first: [slot - S0][lane]
     for (int i = threadIdx.x; i < kLoSlots * 64; i += 64 * kWpb)
@@ -483,13 +500,18 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     load(tn < n_tiles ? tn : t, pre);
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
     f32x4 z;
-    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
-                                       wave_tile_in_bounded<MODE, IN>>(
-        X, FL, lane, fh, fbs, fvs, net.n_classes, z);
+    int lab;
+    if constexpr (kDiff) {
+      lab = wave_tile_label2<KS0, T1, T2, IN, XS, false, wave_tile_in_bounded<MODE, IN>>(
+          X, FL, lane, fh, fbs, fvs, LdsRow{slot_s + g * NSLP + NSL});
+    } else {
+      lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
+                               wave_tile_in_bounded<MODE, IN>>(X, FL, lane, fh, fbs, fvs, net.n_classes, z);
+    }
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) {
       labels[w] = (uint8_t)lab;
-      store_logits(net.logits, w, z, net.n_classes);
+      if constexpr (!kDiff) store_logits(net.logits, w, z, net.n_classes);
     }
   };
   // kPF tiles per trip (VAD_FFN_PF; 1 in the all-LDS residency, whose
@@ -628,12 +650,22 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
         int64_t wblocks = (n_rows + kWpb * kWTile - 1) / (kWpb * kWTile);
         const int64_t wcap = WaveResidency<KS0, NC>::kWavesPerSimd * 4 / kWpb * ffn_num_cus();
         if (wblocks > wcap) wblocks = wcap;
-        if (mode == VAD_FEAT_OFFLINE)
-          hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE>),
-                             dim3((int)wblocks), dim3(64 * kWpb), 0, st, net, in, n_rows, labels);
-        else
-          hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_ANALYSER>),
-                             dim3((int)wblocks), dim3(64 * kWpb), 0, st, net, in, n_rows, labels);
+        const dim3 grid((int)wblocks), blk(64 * kWpb);
+        if (mode == VAD_FEAT_OFFLINE) {
+          if (net.logits)
+            hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE, true>), grid, blk, 0, st,
+                               net, in, n_rows, labels);
+          else
+            hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_OFFLINE, false>), grid, blk, 0, st,
+                               net, in, n_rows, labels);
+        } else {
+          if (net.logits)
+            hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_ANALYSER, true>), grid, blk, 0, st,
+                               net, in, n_rows, labels);
+          else
+            hipLaunchKernelGGL((ffn_wave_kernel<KS0, T1, T2, T3, T4, NC, VAD_FEAT_ANALYSER, false>), grid, blk, 0, st,
+                               net, in, n_rows, labels);
+        }
         return hipGetLastError();
       }
       if (mfcc_n == 13 && net.fragh) {

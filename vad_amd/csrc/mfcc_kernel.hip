@@ -960,16 +960,32 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     return src + (F < flast ? F : flast) * (32 * HOPC);
   };
   // bias and VALU output-layer slots: one value per lane group -> LDS table
+  // (a two-class network with a VALU output layer also gets the logit-
+  // difference slots of valu_label2 after them, as the window kernel does,
+  // so both clip forms classify with the same arithmetic)
+  constexpr bool kDiff = NC == 2 && TP::VL && TP::NL == 3;
+  constexpr int NS = TP::NB + TP::NV + TP::NVB;
+  constexpr int NSD = kDiff ? TP::TIL * 4 + 1 : 0;
   {
-    constexpr int NS = TP::NB + TP::NV + TP::NVB;
-    static_assert(4 * NS <= kSlotTableFloats, "slot table");
-    for (int i = tid; i < 4 * NS; i += kThreads) {
-      const int sl = i >> 2, gg = i & 3;
+    static_assert(4 * (NS + NSD) <= kSlotTableFloats, "slot table");
+    auto slot_val = [&](int sl, int gg) {
       // slots after the biases: the VALU layer's (host order: 4 classes, then biases)
       const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
                                      : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
                                                                                   : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
-      stbl[i] = net.frag[src_sl * 64 + 16 * gg];
+      return net.frag[src_sl * 64 + 16 * gg];
+    };
+    for (int i = tid; i < 4 * (NS + NSD); i += kThreads) {
+      const int sl = i >> 2, gg = i & 3;
+      float v;
+      if (sl < NS) {
+        v = slot_val(sl, gg);
+      } else {  // class 1 minus class 0 (weights, then the bias)
+        const int q = sl - NS;
+        v = q < TP::TIL * 4 ? slot_val(TP::NB + TP::TIL * 4 + q, gg) - slot_val(TP::NB + q, gg)
+                            : slot_val(TP::NB + TP::NV + 1, gg) - slot_val(TP::NB + TP::NV, gg);
+      }
+      stbl[i] = v;
     }
   }
   float* X = reinterpret_cast<float*>(scr + 4 * wave * kGroupScratch);  // waves 0..3: own slice
@@ -1002,9 +1018,15 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
     const LdsSlots fb{stbl + g4};
     const LdsSlots fv{stbl + 4 * TP::NB + g4};
-    f32x4 z;
-    const int lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(
-        X, FL, lane, FragRegs{frh}, fb, fv, net.n_classes, z);
+    int lab;
+    if constexpr (kDiff) {
+      lab = wave_tile_label2<KS0, T1, T2, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(
+          X, FL, lane, FragRegs{frh}, fb, fv, LdsSlots{stbl + 4 * NS + g4});
+    } else {
+      f32x4 z;
+      lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(
+          X, FL, lane, FragRegs{frh}, fb, fv, net.n_classes, z);
+    }
     const int64_t i = fs + (int64_t)tt * kTile - 4 + 16 * wave + (lane & 15);
     if (lane < 16 && i >= wb && i < we) labels[i] = (uint8_t)lab;
   };
