@@ -234,14 +234,17 @@ def test_ffn_split_f16_rescale(torch_cuda, golden):
     """Window labels of networks whose activations overflow f16: the split-f16
     MFMA path reruns such tiles at a power-of-two scale.  Scaling layer l's
     weights by 2^10 and its bias by 2^(10 (l + 1)) scales every activation by
-    a power of two, so the labels are the unscaled network's."""
+    a power of two, so the labels are the unscaled network's.  bl13 at 2^16
+    also takes its layer-1 check (the host's analyser bound on the layer-1
+    inputs, FfnDev::h1_bounded, exceeds 32768 there; at 2^10 the bound holds
+    and the check is skipped)."""
     from vad_amd.ffn import FFNClassifier
     from vad_amd.pipeline import VadPipeline
     w = golden("ffn")
     clip = torch_cuda.from_numpy(w["test_clip"]).cuda()
     m = VadPipeline().mfcc(clip)
-    for prefix, n in (("ref39", 4), ("bl13", 3)):
-        lay = [(W * 2.0 ** 10, b * 2.0 ** (10 * (i + 1)))
+    for prefix, n, e in (("ref39", 4, 10), ("bl13", 3, 10), ("bl13", 3, 16)):
+        lay = [(W * 2.0 ** e, b * 2.0 ** (e * (i + 1)))
                for i, (W, b) in enumerate(layers_from(w, prefix, n))]
         got = FFNClassifier(lay).plan.window_labels(m).cpu().numpy()
         sure = w[f"test_margin_{prefix}"] > MARGIN_TOL

@@ -147,9 +147,6 @@ struct vad_mfcc_plan {
   bool generic() const { return fft_n != kFftN; }
 };
 
-// The spec a launch passes: a windowed plan whose bank is a compiled one
-// says which (kSpecWindow26 / 40), so the reference framing keeps the
-// generated mel code; vad_mfcc_plan_variant still reports kSpecWindow.
 // n_hops > 1 blocks of n_streams hop rows: disjoint in either ordering
 // (hop-major: each block past the previous block's last row; stream-major:
 // each row's K hops before the next row), never repeating (block stride > 0)
@@ -160,6 +157,9 @@ static bool vad_hop_layout_disjoint(int64_t n_streams, int32_t n_hops, int64_t b
   return hop_stride >= (int64_t)(n_hops - 1) * block_stride + hop_len;
 }
 
+// The spec a launch passes: a windowed plan whose bank is a compiled one
+// says which (kSpecWindow26 / 40), so the reference framing keeps the
+// generated mel code; vad_mfcc_plan_variant still reports kSpecWindow.
 static int launch_spec(const vad_mfcc_plan* p) {
   if (p->spec != kSpecWindow) return p->spec;
   return p->table_spec == 1 ? kSpecWindow26 : p->table_spec == 2 ? kSpecWindow40 : kSpecWindow;
@@ -538,6 +538,21 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
   wraw.insert(wraw.end(), 3 * 64 + 4, 0.f);
   while (wraw.size() % 4) wraw.push_back(0.f);
   net.wraw_n = (int)wraw.size();
+  // layer-1 inputs of a 13-input network on analyser features (|Mn| <=
+  // sqrt(5), ffn_dev.h wave_tile_in_bounded): bounded by max_j |b0_j| +
+  // sqrt(5) sum_k |W0[k][j]|; a bound under 32768 leaves 2x headroom to the
+  // f16 range for the split-f16 rounding of layer 0 (the check it skips only
+  // ever answers "scale 1" then)
+  net.h1_bounded = 0;
+  if (n_layers >= 2 && dims[0] == 13) {
+    double worst = 0.0;
+    for (int j = 0; j < dims[1]; ++j) {
+      double acc = fabs((double)b[0][j]);
+      for (int k = 0; k < dims[0]; ++k) acc += sqrt(5.0) * fabs((double)W[0][(size_t)k * dims[1] + j]);
+      worst = acc > worst ? acc : worst;
+    }
+    net.h1_bounded = worst < 32768.0 ? 1 : 0;
+  }
 
   vad_ffn_plan* p = (vad_ffn_plan*)calloc(1, sizeof(vad_ffn_plan));
   if (!p) return VAD_ENOMEM;

@@ -381,9 +381,11 @@ __device__ __forceinline__ void acts_of(const f32x4 (&h)[TI], float (&v)[(TI + 1
 // v (scaled by sc, see layer_scale); the TO accumulator chains interleave.
 // BOUNDED: the caller guarantees every input is finite and < 65504 in
 // magnitude, or an infinity (layer_scale's answer is 1 then too): no check.
+// bounded_rt: the same guarantee known at run time (wave-uniform).
 template <int TO, int KS, class FB, bool NONNEG = false, bool MERGE0 = false, bool BOUNDED = false, class FH>
-__device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu) {
-  const float sc = BOUNDED ? 1.f : layer_scale<KS, NONNEG>(v);
+__device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&out)[TO], bool relu,
+                                         bool bounded_rt = false) {
+  const float sc = (BOUNDED || bounded_rt) ? 1.f : layer_scale<KS, NONNEG>(v);
   h8 bh[KS], bl[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
@@ -547,8 +549,11 @@ __device__ __forceinline__ f32x4 mlp_forward_h3(FH fh, FB fb, FV fv, float (&x0)
 // The hidden layers of a three-layer split-f16 network whose output layer
 // runs on the VALU (13-64-64-2): the last hidden layer's accumulator tiles,
 // for valu_label2.
+// h1_bounded (FfnDev::h1_bounded, meaningful with IN_BOUNDED inputs): layer
+// 1 skips its f16-range check too.
 template <int KS0, int T1, int T2, class FB, bool IN_BOUNDED, class FH>
-__device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS0 + 31) / 32][8], f32x4 (&h2)[T2]) {
+__device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS0 + 31) / 32][8], f32x4 (&h2)[T2],
+                                               bool h1_bounded) {
   using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
   using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
   static_assert(TP::NL == 3 && TP::VL, "three layers, the output layer on the VALU");
@@ -556,7 +561,7 @@ __device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS
   dense_h3<T1, HP::K0, FB, false, kMerge0<KS0>, IN_BOUNDED>(fh, fb, x0, h1, true);
   float v1[HP::K1][8];
   acts_of<T1>(h1, v1);
-  dense_h3<T2, HP::K1, FB, true>(fh.at(HP::S0), fb + 4 * T1, v1, h2, true);
+  dense_h3<T2, HP::K1, FB, true>(fh.at(HP::S0), fb + 4 * T1, v1, h2, true, IN_BOUNDED && h1_bounded);
 }
 
 // Per-lane fragment slots read straight from global memory (L1 / L2
@@ -720,13 +725,13 @@ __device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, c
 // difference slots (TI*4 weights, then the bias).
 template <int KS0, int T1, int T2, int IN, int XS, bool MASK, bool IN_BOUNDED, class FH, class FB, class FV, class FD>
 __device__ __forceinline__ int wave_tile_label2(const float* __restrict__ X, const int* __restrict__ FL, int lane,
-                                                FH fh, FB fb, FV fv, FD fd) {
+                                                FH fh, FB fb, FV fv, FD fd, int h1_bounded) {
   constexpr int K0 = (4 * KS0 + 31) / 32;
   using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
   float x0[K0][8];
   const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
   f32x4 h2[T2];
-  mlp_hidden2_h3<KS0, T1, T2, FB, IN_BOUNDED>(fh, fb, x0, h2);
+  mlp_hidden2_h3<KS0, T1, T2, FB, IN_BOUNDED>(fh, fb, x0, h2, h1_bounded != 0);
   return valu_label2<TP, T2>(fd, fv, h2, wnan);
 }
 

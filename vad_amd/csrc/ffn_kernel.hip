@@ -503,7 +503,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     int lab;
     if constexpr (kDiff) {
       lab = wave_tile_label2<KS0, T1, T2, IN, XS, false, wave_tile_in_bounded<MODE, IN>>(
-          X, FL, lane, fh, fbs, fvs, LdsRow{slot_s + g * NSLP + NSL});
+          X, FL, lane, fh, fbs, fvs, LdsRow{slot_s + g * NSLP + NSL}, net.h1_bounded);
     } else {
       lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
                                wave_tile_in_bounded<MODE, IN>>(X, FL, lane, fh, fbs, fvs, net.n_classes, z);

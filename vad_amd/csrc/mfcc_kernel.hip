@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
     int lab;
     if constexpr (kDiff) {
       lab = wave_tile_label2<KS0, T1, T2, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(
-          X, FL, lane, FragRegs{frh}, fb, fv, LdsSlots{stbl + 4 * NS + g4});
+          X, FL, lane, FragRegs{frh}, fb, fv, LdsSlots{stbl + 4 * NS + g4}, net.h1_bounded);
     } else {
       f32x4 z;
       lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, false, IN, XS, true, wave_tile_in_bounded<MODE, IN>>(

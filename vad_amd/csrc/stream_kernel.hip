@@ -189,28 +189,26 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
                                                           int64_t hop_kstride, int64_t lab_kstride) {
   extern __shared__ __attribute__((aligned(16))) float hsm[];
   const int waves = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   // -- stage the plans' tables (the MFCC plan's hop blob, then the FFN
-  // weights) with 16-B loads, all issued before any store: one L2 round
-  // trip, then the block's only barrier
+  // weights) by LDS-DMA (global_load_lds_dwordx4: 1 KB per wave-instruction,
+  // no registers, all in flight at once), then request the stream's state
+  // and the FFT's twiddles (registers), then the block's only barrier.
+  // (A/B, 512 streams, profiles/r05/ab/hop_staging_ab.json: 10.26 us per
+  // one-hop launch against 10.56 for register staging with LDS twiddles;
+  // the barrier moved after the first hop's FFT, so that the staging would
+  // overlap it, measured 10.84: the mid-hop barrier costs more than it hides)
   float* base = hsm + waves * kHopWaveFloats;
   {
     const float4* m4 = reinterpret_cast<const float4*>(blob);
     const float4* w4 = reinterpret_cast<const float4*>(net.wraw);
-    float4* d4 = reinterpret_cast<float4*>(base);
     const int nm4 = blob_n >> 2, n4 = nm4 + (net.wraw_n >> 2);
-    constexpr int kQ = VAD_HOP_Q;  // 16-B loads in flight per thread
-    for (int i0 = 0; i0 < n4; i0 += kQ * (int)blockDim.x) {
-      float4 t[kQ];
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) {
-        const int i = i0 + q * blockDim.x + threadIdx.x;
-        t[q] = i < nm4 ? m4[i] : (i < n4 ? w4[i - nm4] : make_float4(0.f, 0.f, 0.f, 0.f));
-      }
-#pragma unroll
-      for (int q = 0; q < kQ; ++q) {
-        const int i = i0 + q * blockDim.x + threadIdx.x;
-        if (i < n4) d4[i] = t[q];
-      }
+    for (int c0 = wv * 64; c0 < n4; c0 += (int)blockDim.x) {  // wave-uniform chunk base
+      const int c = c0 + lane;
+      if (c < n4)
+        __builtin_amdgcn_global_load_lds(c < nm4 ? (const void*)(m4 + c) : (const void*)(w4 + (c - nm4)),
+                                         (__attribute__((address_space(3))) void*)(base + 4 * c0), 16, 0, 0);
     }
   }
   HopTables T;
@@ -223,14 +221,12 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   T.dct = T.taps + n_taps;
   T.w = base + blob_n;
 
-  const int lane = threadIdx.x & 63;
-  const int wv = threadIdx.x >> 6;
   const int64_t s = (int64_t)blockIdx.x * waves + wv;
   const int64_t sc = s < n_streams ? s : 0;
   // -- the stream's state, requested before the barrier so its latency
-  // overlaps the staging: the frame as it stands (registers, sample
-  // t = lane + 64 i), the first hop's new samples at the positions they take
-  // in the advanced frame, the frame count and the MFCC ring
+  // overlaps the staging: the frame as it stands (registers, sample t =
+  // lane + 64 i), the first hop's new samples at the positions they take in
+  // the advanced frame, the frame count and the MFCC ring
   float* row = frames + sc * fstride;
   const int keep = len - hlen;
   float v[NR], hn[NR];
@@ -245,7 +241,26 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   float rv[5];
 #pragma unroll
   for (int d = 0; d < 5; ++d) rv[d] = lane < mfcc_n ? rs[d * mfcc_n + lane] : 0.f;
-  __syncthreads();
+  // this lane's FFT twiddles (W512^k table = the blob's first 256 complex):
+  // stage st's radix-4 butterfly multiplies by W256^(j m), m = (lane mod
+  // 4^st) 64 / 4^st, j = 1..3; the real-FFT split by W512^(lane + 64 q)
+  // (the 16-chunk build, whose frame registers leave no room for them, reads
+  // them from the staged table where it uses them)
+  const float2* tw_g = reinterpret_cast<const float2*>(blob);
+  constexpr bool kTwReg = NR <= 7;
+  float2 twr[3][3], tws[4];
+  if constexpr (kTwReg) {
+#pragma unroll
+    for (int st = 1; st < 4; ++st) {
+      const int ns = 1 << (2 * st);
+      const int m = (lane & (ns - 1)) * (64 >> (2 * st));
+#pragma unroll
+      for (int jj = 1; jj < 4; ++jj) twr[st - 1][jj - 1] = w256(tw_g, jj * m);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) tws[q] = tw_g[lane + 64 * q];
+  }
+  __syncthreads();  // the staged tables are complete (the barrier waits for the LDS-DMA)
   if (s >= n_streams) return;  // wave-uniform; no barrier below
   float* scr = hsm + wv * kHopWaveFloats;
   float2* z0 = reinterpret_cast<float2*>(scr);
@@ -307,11 +322,11 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       const int ns = 1 << (2 * st);  // 1, 4, 16, 64
       const int kk = ln & (ns - 1);
       float2 a0 = src[zp(ln)], a1 = src[zp(ln + 64)], a2 = src[zp(ln + 128)], a3 = src[zp(ln + 192)];
-      if (st > 0) {
-        const int m = kk * (64 >> (2 * st));  // W_{4 ns}^k = W256^(64 k / ns)
-        a1 = cmulf(a1, w256(T.tw, m));
-        a2 = cmulf(a2, w256(T.tw, 2 * m));
-        a3 = cmulf(a3, w256(T.tw, 3 * m));
+      if (st > 0) {  // W_{4 ns}^(j k) = W256^(64 j k / ns)
+        const int m = kk * (64 >> (2 * st));
+        a1 = cmulf(a1, kTwReg ? twr[st - 1][0] : w256(T.tw, m));
+        a2 = cmulf(a2, kTwReg ? twr[st - 1][1] : w256(T.tw, 2 * m));
+        a3 = cmulf(a3, kTwReg ? twr[st - 1][2] : w256(T.tw, 3 * m));
       }
       const float2 b0 = make_float2(a0.x + a2.x, a0.y + a2.y), b1 = make_float2(a0.x - a2.x, a0.y - a2.y);
       const float2 b2 = make_float2(a1.x + a3.x, a1.y + a3.y), b3 = make_float2(a1.x - a3.x, a1.y - a3.y);
@@ -335,7 +350,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
       const float2 zk = src[zp(kb)], zn = src[zp((256 - kb) & 255)];
       const float2 S = make_float2(zk.x + zn.x, zk.y - zn.y);
       const float2 D = make_float2(zk.x - zn.x, zk.y + zn.y);
-      const float2 Tw = cmulf(D, T.tw[kb]);
+      const float2 Tw = cmulf(D, kTwReg ? tws[q] : T.tw[kb]);
       const float u = S.x + Tw.y, vv = S.y - Tw.x;
       pk[q] = fmaf(u, u, vv * vv);
     }

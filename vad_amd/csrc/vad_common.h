@@ -68,6 +68,11 @@ struct FfnDev {
   int wraw_n;  // floats in wraw
   int woff[VAD_MAX_FFN_LAYERS];
   int boff[VAD_MAX_FFN_LAYERS];
+  // 1: with analyser inputs (|Mn| <= sqrt(5), or a NaN / inf the kernels
+  // handle as they come) every finite layer-1 input is below 32768 in
+  // magnitude, so that layer needs no f16-range check (capi.hip, from the
+  // layer-0 weights: max_j |b_j| + sqrt(5) sum_k |W[k][j]|)
+  int h1_bounded;
 };
 
 // Decision-tree node (tree_kernel.hip): internal if feature >= 0 (go left
