@@ -305,9 +305,9 @@ int vad_stream_hop(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* fr
  * n_hops < 0, or n_hops > 1 with label_block_stride < n_streams, or with
  * hop rows that repeat or overlap: hop_block_stride must be > 0 and the rows
  * disjoint in one of the two orderings, hop-major (hop_block_stride >=
- * (n_streams - 1) * hop_stride + hop_len) or stream-major (hop_stride >=
- * (n_hops - 1) * hop_block_stride + hop_len, e.g. an (S, K * hop) buffer
- * viewed as (K, S, hop)). */
+ * (n_streams - 1) * hop_stride + hop_len) or stream-major (hop_block_stride
+ * >= hop_len and hop_stride >= (n_hops - 1) * hop_block_stride + hop_len,
+ * e.g. an (S, K * hop) buffer viewed as (K, S, hop)). */
 int vad_stream_hops(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, float* frames, int64_t frame_stride,
                     int32_t frame_len, const float* hop, int64_t hop_stride, int32_t hop_len, int64_t n_streams,
                     int32_t n_hops, int64_t hop_block_stride, float* ring, int32_t* count, uint8_t* labels,

@@ -251,6 +251,83 @@ def test_ffn_split_f16_rescale(torch_cuda, golden):
         np.testing.assert_array_equal(got[sure], w[f"test_labels_{prefix}"][sure])
 
 
+def test_ffn_label_difference_overflowed_logits(torch_cuda):
+    """The labels-only launches of a 13-64-64-2 network decide by the logit
+    difference d = z1 - z0 (ffn_dev.h valu_label2) and rerun a wave's 16
+    windows (tile t: windows 16 t .. 16 t + 15) in the two-logit form when
+    some d is not finite.  Scaling layer 1 by 2^16 and the output layer by
+    2^112 (every weight within f16 / f32 range) pushes many windows' f32
+    logits past 2^128:
+      * output columns mixed 0.95 / 0.05 (correlated logits, small
+        difference weights): in tiles where no partial sum of d can overflow
+        (sum_k |fd_k h_k| < 2^127.5, fp64), the labels are the fp64 oracle's
+        (the sign of z1 - z0) even where the f32 logits are infinite -- where
+        argmax of the two-logit form is arbitrary (an overflowed partial sum
+        of z0 can even give +inf for a negative exact z0);
+      * unmixed: in tiles where some |d| exceeds 1.01 * 2^128 (d overflows
+        in any f32 order), every window carries the logits launch's label
+        (vad_features_ffn_logits: the same two-logit code and argmax rules);
+      * finite logits apart from f32 near-ties: both launches agree;
+        NaN-flagged windows are class 0; the fused kernel agrees with both
+        there."""
+    from vad_amd import plan as P
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    F = 20000
+    clip = O.synth_clip(160 * (F - 1) + 401, seed=11).astype(np.float32)
+    a = torch_cuda.from_numpy(clip).cuda()
+    m = VadPipeline().mfcc(a)
+    x = P.window_features(m, 0).cpu().numpy()[:, :13].astype(np.float64)
+    flag = np.isnan(x).any(axis=1)
+    nt = (len(x) + 15) // 16
+
+    def per_tile_max(v):
+        p = np.zeros(nt * 16)
+        p[:len(v)] = np.nan_to_num(np.where(flag, 0.0, v))
+        return np.repeat(p.reshape(nt, 16).max(axis=1), 16)[:len(v)]
+
+    for mix in (0.95, 0.0):
+        lay = random_layers(TOPOLOGY_BL13, seed=5)
+        W, b = lay[-1]
+        W = W.copy()
+        W[:, 1] = mix * W[:, 0] + (1 - mix) * W[:, 1]
+        lay = lay[:-1] + [(W, b)]
+        lay_s = [lay[0], tuple((t * 2.0 ** 16).astype(np.float32) for t in lay[1]),
+                 tuple((t * 2.0 ** 112).astype(np.float32) for t in lay[2])]
+        clf = FFNClassifier(lay_s)
+        lab = clf.plan.window_labels(m).cpu().numpy()
+        lab_l, zl = (t.cpu().numpy() for t in P.window_logits(clf.plan, m))
+        np.testing.assert_array_equal(lab[flag], 0)
+        # fp64 hidden activations of the scaled network, and the device's f32
+        # difference weights (class 1 minus class 0 of the f32 plan weights)
+        h = x
+        for Wl, bl in lay_s[:2]:
+            h = O.relu_keep_nan(h @ Wl.astype(np.float64) + bl.astype(np.float64))
+        W2, b2 = lay_s[2]
+        fd = (W2[:, 1] - W2[:, 0]).astype(np.float64)
+        d64 = h @ fd + float(b2[1] - b2[0])
+        quiet = per_tile_max(np.abs(h) @ np.abs(fd)) < 2.0 ** 127.5
+        rerun = per_tile_max(np.abs(d64)) > 1.01 * 2.0 ** 128
+        big = ~np.isfinite(zl).all(axis=1) & ~flag
+        with np.errstate(over="ignore", invalid="ignore"):
+            fin = np.isfinite(zl).all(axis=1) & ~flag
+            rel = fin & (np.abs(zl[:, 1] - zl[:, 0]) > 1e-5 * np.abs(zl).max(axis=1))
+        np.testing.assert_array_equal(lab[rel], lab_l[rel])
+        sure = np.abs(d64) > 1e-5 * np.abs(h @ W2.astype(np.float64)).max(axis=1)
+        ref = (d64 > 0).astype(np.uint8)  # argmax of two finite fp64 logits
+        sel = quiet & sure & ~flag
+        np.testing.assert_array_equal(lab[sel], ref[sel])
+        np.testing.assert_array_equal(lab[rerun], lab_l[rerun])
+        if mix == 0.95:
+            assert (sel & big).sum() > 1000, int((sel & big).sum())
+        else:
+            assert (rerun & big).sum() > 1000, int((rerun & big).sum())
+        # the fused kernel (its own tiles) on bit-identical MFCC rows
+        lab_f = VadPipeline(clf).labels(a, fused=True).cpu().numpy()
+        det = flag | rel
+        np.testing.assert_array_equal(lab_f[det], lab[det])
+
+
 def test_window_labels_random_nets_long_clip(torch_cuda):
     """Window labels of both specialised topologies (split-f16 MFMA path; a
     3-class 13-64-64-3 runs the bl13 shape with its fragments in LDS) on a

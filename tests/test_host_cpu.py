@@ -224,3 +224,4 @@ def test_hop_rows_disjoint_layouts():
     assert not hop_rows_disjoint(S, K, -S * H, H, H)       # backwards
     assert not hop_rows_disjoint(S, K, 3 * H, H, H)        # blocks overlap
     assert not hop_rows_disjoint(S, K, H, K * H - 1, H)    # stream rows overlap
+    assert not hop_rows_disjoint(S, K, H - 1, K * H, H)    # a stream's hops overlap each other

@@ -1,0 +1,97 @@
+"""Property-based (hypothesis) tests of the host logic, CPU only.
+
+  split_clip     the shards of a clip partition its F - 5 windows in rank
+                 order, each segment (with its 240-sample + 4-frame halo,
+                 SURVEY 8(e)) frames to exactly its own windows, and the
+                 oracle's labels of the segments concatenate to the oracle's
+                 labels of the whole clip (the halo rule, end to end)
+  hop layouts    hop_rows_disjoint (stream.py; capi.hip's
+                 vad_hop_layout_disjoint is the same rule) only accepts
+                 layouts whose K x S hop rows are pairwise disjoint (checked
+                 by brute force, for row strides >= the hop length, which
+                 the C ABI requires first), and accepts both contiguous
+                 orderings
+"""
+import numpy as np
+import pytest
+
+from oracle import vad_oracle as O
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+FUZZ = settings(max_examples=200, deadline=None, derandomize=True, database=None)
+
+
+@FUZZ
+@given(n=st.integers(0, 2_000_000), world=st.integers(1, 8))
+def test_split_clip_partitions_windows(n, world):
+    from vad_amd.dist import n_frames, split_clip
+    n_win = max(n_frames(n) - 5, 0)
+    assert n_frames(n) == O.n_frames(n)
+    nxt = 0
+    for r in range(world):
+        sh = split_clip(n, r, world)
+        assert sh.win_lo == nxt and sh.win_hi >= sh.win_lo
+        nxt = sh.win_hi
+        if sh.n_windows:
+            assert 0 <= sh.sample_lo < sh.sample_hi <= n
+            assert sh.sample_lo == 160 * sh.win_lo  # window w starts at frame w
+            assert max(n_frames(sh.sample_hi - sh.sample_lo) - 5, 0) == sh.n_windows
+    assert nxt == n_win
+
+
+@settings(FUZZ, max_examples=25)
+@given(frames=st.integers(0, 60), extra=st.integers(0, 159), world=st.integers(1, 5),
+       seed=st.integers(0, 2 ** 31))
+def test_split_clip_labels_concatenate(frames, extra, world, seed):
+    from vad_amd.dist import split_clip
+    from vad_amd.ffn import TOPOLOGY_BL13, random_layers
+    n = 160 * frames + 241 + extra if frames else extra
+    clip = O.synth_clip(n, seed=seed, segment=400)
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    lay = random_layers(TOPOLOGY_BL13, seed=1)
+
+    def labels(x):
+        if O.n_frames(len(x)) <= 5:
+            return np.zeros((0,), np.int64)
+        f = O.analyser_features_fast(O.mfcc_batch(x, fb))[:, :13]
+        return O.ffn_labels(f, lay)
+
+    whole = labels(clip)
+    parts = []
+    for r in range(world):
+        sh = split_clip(n, r, world)
+        if sh.n_windows:
+            part = labels(clip[sh.sample_lo:sh.sample_hi])
+            assert len(part) == sh.n_windows
+            parts.append(part)
+    got = np.concatenate(parts) if parts else np.zeros((0,), np.int64)
+    np.testing.assert_array_equal(got, whole)
+
+
+def _rows_disjoint_brute(S, K, block, hs, hl):
+    starts = sorted(k * block + s * hs for k in range(K) for s in range(S))
+    return all(b - a >= hl for a, b in zip(starts, starts[1:]))
+
+
+@FUZZ
+@given(S=st.integers(1, 12), K=st.integers(1, 9), hl=st.integers(1, 200),
+       block=st.integers(-3000, 3000), gap=st.integers(0, 3000))
+def test_hop_rows_disjoint_is_sound(S, K, block, gap, hl):
+    """Rows of one hop never overlap: vad_stream_hops rejects hop_stride <
+    hop_len before this rule applies, so the row stride is hl + gap."""
+    from vad_amd.stream import hop_rows_disjoint
+    hs = hl + gap
+    if hop_rows_disjoint(S, K, block, hs, hl):
+        assert _rows_disjoint_brute(S, K, block, hs, hl)
+
+
+@FUZZ
+@given(S=st.integers(1, 64), K=st.integers(1, 16), hl=st.integers(1, 400), pad=st.integers(0, 64))
+def test_hop_rows_disjoint_accepts_contiguous_orderings(S, K, hl, pad):
+    from vad_amd.stream import hop_rows_disjoint
+    row = hl + pad
+    assert hop_rows_disjoint(S, K, S * row, row, hl)   # (K, S, row): hop-major
+    assert hop_rows_disjoint(S, K, row, K * row, hl)   # (S, K * row): stream-major

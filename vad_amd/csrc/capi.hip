@@ -154,7 +154,8 @@ static bool vad_hop_layout_disjoint(int64_t n_streams, int32_t n_hops, int64_t b
                                     int32_t hop_len) {
   if (block_stride <= 0) return false;
   if (block_stride >= (n_streams - 1) * hop_stride + hop_len) return true;
-  return hop_stride >= (int64_t)(n_hops - 1) * block_stride + hop_len;
+  // stream-major: a stream's K hops apart from each other, then the next stream
+  return block_stride >= hop_len && hop_stride >= (int64_t)(n_hops - 1) * block_stride + hop_len;
 }
 
 // The spec a launch passes: a windowed plan whose bank is a compiled one

@@ -75,6 +75,7 @@ class MfccPlan:
                                           self.fft_n, self.mfcc_n, int(lifter_L), ctypes.byref(h)),
               "vad_mfcc_plan_create")
         self._h = h
+        self._destroy = lib().vad_mfcc_plan_destroy
 
     @classmethod
     def from_config(cls, cfg: MfccConfig = MfccConfig()):
@@ -111,8 +112,9 @@ class MfccPlan:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.vad_mfcc_plan_destroy(h)
+        destroy = getattr(self, "_destroy", None)  # bound at creation: module globals
+        if h is not None and h.value and destroy is not None:  # may be gone at exit
+            destroy(h)
             self._h = None
 
     # -- frame sources ------------------------------------------------------
@@ -189,6 +191,7 @@ class FfnPlan:
         h = ctypes.c_void_p()
         check(lib().vad_ffn_plan_create(n, d, wp, bp, ctypes.byref(h)), "vad_ffn_plan_create")
         self._h = h
+        self._destroy = lib().vad_ffn_plan_destroy
 
     @property
     def handle(self):
@@ -214,8 +217,9 @@ class FfnPlan:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.vad_ffn_plan_destroy(h)
+        destroy = getattr(self, "_destroy", None)  # bound at creation: module globals
+        if h is not None and h.value and destroy is not None:  # may be gone at exit
+            destroy(h)
             self._h = None
 
     def predict(self, x, out=None, stream=None):

@@ -54,7 +54,7 @@ def hop_rows_disjoint(n_streams, n_hops, block_stride, hop_stride, hop_len):
     if block_stride <= 0:
         return False
     return (block_stride >= (n_streams - 1) * hop_stride + hop_len
-            or hop_stride >= (n_hops - 1) * block_stride + hop_len)
+            or (block_stride >= hop_len and hop_stride >= (n_hops - 1) * block_stride + hop_len))
 
 
 class StreamBatch:

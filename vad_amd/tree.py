@@ -43,6 +43,7 @@ class TreePlan:
                                          rt.ctypes.data, lf.ctypes.data, nl.ctypes.data,
                                          int(n_features), ctypes.byref(h)), "vad_tree_plan_create")
         self._h = h
+        self._destroy = lib().vad_tree_plan_destroy
         self.n_features = int(n_features)
 
     @property
@@ -51,8 +52,9 @@ class TreePlan:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h is not None and h.value and _lib._lib is not None:
-            _lib._lib.vad_tree_plan_destroy(h)
+        destroy = getattr(self, "_destroy", None)  # bound at creation: module globals
+        if h is not None and h.value and destroy is not None:  # may be gone at exit
+            destroy(h)
             self._h = None
 
 
