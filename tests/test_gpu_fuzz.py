@@ -37,7 +37,7 @@ pytestmark = pytest.mark.gpu
 
 MFCC_TOL = 1e-4
 MARGIN_TOL = 0.05
-FUZZ = settings(max_examples=40, deadline=None, derandomize=True, database=None,
+FUZZ = settings(max_examples=120, deadline=None, derandomize=True, database=None,
                 suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 
 
@@ -124,7 +124,7 @@ def test_fuzz_clip_path(torch_cuda, nets, n, log_amp, seed, silence, i16, offlin
     np.testing.assert_array_equal(lab[ok], O.ffn_labels(x, lay)[ok])
 
 
-@settings(FUZZ, max_examples=25)
+@settings(FUZZ, max_examples=50)
 @given(S=st.integers(1, 70), T=st.integers(6, 40), K=st.sampled_from([1, 2, 3, 8]),
        log_amp=st.floats(-1.0, 4.6), seed=st.integers(0, 2 ** 32 - 1), kernel=st.sampled_from(["hop", "three"]),
        graph=st.booleans())
