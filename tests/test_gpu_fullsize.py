@@ -283,6 +283,41 @@ def test_clip_past_2g_samples(torch_cuda):
     torch.cuda.empty_cache()
 
 
+def test_clip_past_2g_mfcc_values(torch_cuda):
+    """Maximum-size edge, one step further: 170M frames of int16 PCM (27.2e9
+    samples, 54 GB on the device; 8.8 GB of MFCC rows) put the MFCC row
+    element index 13 f past 2^31 (at frame 165,191,050) and the window
+    index of the FFN and fused kernels past 2^27 tiles.  As above, frames cut
+    out of the big clip at its start, across that boundary and at its end
+    give bit-identical MFCCs and labels as small clips; the fused kernel's
+    labels equal the two-kernel labels over the whole clip."""
+    torch = torch_cuda
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.pipeline import VadPipeline
+    free, _ = torch.cuda.mem_get_info()
+    if free < 100 << 30:
+        pytest.skip("needs ~100 GB of free device memory")
+    F = 170_000_000
+    n = 160 * (F - 1) + 401
+    assert 13 * F > 2 ** 31
+    g = torch.Generator(device="cuda").manual_seed(78)
+    a16 = torch.randint(-32767, 32768, (n,), dtype=torch.int16, device="cuda", generator=g)
+    a16[160 * (F - 3000): 160 * (F - 2000)] = 0  # digital silence near the end: NaN windows
+    pipe = VadPipeline(FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3)))
+    assert pipe.fusable
+    big = pipe.mfcc(a16)
+    big_lab = pipe.labels(a16)
+    assert torch.equal(pipe.labels(a16, fused=True), big_lab)
+    W = 4000  # frames per cut
+    for f0 in (0, (2 ** 31) // 13 - W // 2, F - W):
+        cut = a16[160 * f0: 160 * (f0 + W - 1) + 401].contiguous()
+        assert torch.equal(pipe.mfcc(cut), big[f0:f0 + W]), f0
+        assert torch.equal(pipe.labels(cut), big_lab[f0:f0 + W - 5]), f0
+    assert (big_lab[F - 2990: F - 2010] == 0).all()  # windows inside the silence
+    del a16, big, big_lab
+    torch.cuda.empty_cache()
+
+
 def test_kernel_time_guard(torch_cuda):
     """A coarse regression guard on the benchmark kernels (C3 sizes, 1M
     frames), reported rather than tuned: the median over 7 batches of 20
