@@ -217,6 +217,49 @@ def test_c5_512_streams_graph_replay(torch_cuda, golden, kernel):
     assert int((got[:, 5:] != ref_l).sum()) <= 2
 
 
+def test_stream_hops_100k_streams(torch_cuda, golden):
+    """Maximum-size edge of the streaming path: 100,000 live streams (16
+    streams per block, 6,250 blocks), 8 hops as one vad_stream_hops launch
+    and as 8 one-hop launches on a second batch: identical labels, frames,
+    rings and counts; every 997th stream's labels vs the oracle's (margin
+    rule) and its frame buffer equal to the last 400 samples it was fed."""
+    torch = torch_cuda
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.stream import StreamBatch
+    w = golden("ffn")
+    layers = [(w[f"ref39_W{i}"], w[f"ref39_b{i}"]) for i in range(4)]
+    S, T = 100_000, 8
+    n = 160 * (T - 1) + 401
+    g = torch.Generator(device="cuda").manual_seed(79)
+    amp = 10.0 ** (4 * torch.rand((S, 1), generator=g, device="cuda"))
+    clips = (torch.randn((S, n), generator=g, device="cuda") * amp).round_().clamp_(-32767, 32767)
+    hops = clips[:, 240:240 + 160 * T].reshape(S, T, 160).transpose(0, 1).contiguous()  # (T, S, 160)
+    clf = FFNClassifier(layers)
+    blk = StreamBatch(S, clf, kernel="hop", hops_per_step=T)
+    one = StreamBatch(S, clf, kernel="hop")
+    for sb in (blk, one):
+        sb.prime(clips[:, :240].contiguous())
+    lab_blk = blk.step_block(hops).clone()  # (T, S)
+    lab_one = torch.stack([one.step(hops[t]).clone() for t in range(T)])
+    assert torch.equal(lab_blk, lab_one)
+    for a, b in ((blk.frames, one.frames), (blk.ring, one.ring), (blk.count, one.count)):
+        assert torch.equal(a, b)
+    assert torch.equal(blk.frames, clips[:, n - 401: n - 1])  # the last frame fed: samples 160 (T-1) ..
+    assert (lab_blk[:5] == 255).all()
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    got = lab_blk[5:].cpu().numpy()  # (T - 5, S)
+    n_ok = 0
+    for s in range(0, S, 997):
+        c = clips[s].cpu().numpy()  # T frames (strict '>' framing): windows 0 .. T - 6
+        x = O.analyser_features_fast(O.mfcc_batch(c, fb))
+        ok = O.ffn_margin(x, layers) > LABEL_MARGIN
+        np.testing.assert_array_equal(got[:, s][ok], O.ffn_labels(x, layers)[ok])
+        n_ok += int(ok.sum())
+    assert n_ok > 0.9 * 3 * len(range(0, S, 997))
+    del clips, hops, blk, one
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("topo", [(13, 64, 64, 2), (39, 64, 32, 16, 3)])
 def test_split_f16_logit_error_bounded(torch_cuda, topo):
     """The split-f16 MFMA forward (hi*hi + hi*lo + lo*hi, lo*lo dropped)
