@@ -58,7 +58,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the driver's C4 world size, rehearsed on gloo
 def test_gather_labels_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -118,7 +118,7 @@ def _oracle_shard_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_clip_labels_equal_whole_clip(world):
     """The halo rule on the CPU oracle: every rank classifies its segment,
     the gathered labels are the whole clip's (windows at every cut included)."""
@@ -153,7 +153,7 @@ def _warmup_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_warmup_continuation_agreed_across_ranks(world):
     """Regression (the 2-rank bench rehearsal hung when the ranks' time-based
     warm-up ran different numbers of gathering steps): with any_rank every
