@@ -1,5 +1,5 @@
-"""Multi-process paths on the GPU box (one MI355X): two ranks sharing cuda:0
-over gloo run the real HIP pipeline on their shard of one clip (the 240-sample
+"""Multi-process paths on the GPU box (one MI355X): 2, 3 or 8 ranks sharing
+cuda:0 over gloo run the real HIP pipeline on their shard of one clip (the 240-sample
 + 4-frame halo rule) and the gathered labels equal the single-process labels;
 a world-size-1 RCCL ("nccl") group runs the label gather bench.py uses.
 
@@ -65,7 +65,7 @@ def _shard_worker(rank, world, port, q):
         raise
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: C4's world size, all ranks on cuda:0
 def test_clip_shards_on_one_gpu_match_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
