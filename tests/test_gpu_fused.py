@@ -52,6 +52,42 @@ def test_fused_equals_two_kernel(torch_cuda, topo):
                                                 int((got != want).sum()))
 
 
+def test_fused_independent_of_stale_lds(torch_cuda):
+    """The fused kernel's first tile has no previous tile: ring rows 0..3
+    (the halo of windows before the workgroup's first, never stored) share
+    wave 0's 16-window tile with stored windows.  They are zeroed, not left
+    as whatever an earlier kernel wrote to that LDS: stale values past f16
+    range would force the tile's split-f16 rescale and perturb its real
+    windows (found by tests/test_gpu_fuzz.py on a box whose LDS held such
+    values).  Here a test-only kernel (tests/c_host/lds_poison.hip) fills
+    every CU's 160 KB of LDS with 1e30 right before each fused launch; the
+    fused labels must still equal the two-kernel labels, for short clips (one
+    workgroup, its first tile only) in both feature forms."""
+    import ctypes
+    import os
+    torch = torch_cuda
+    so = os.path.join(os.path.dirname(os.path.abspath(__file__)), "c_host", "liblds_poison.so")
+    if not os.path.exists(so):
+        pytest.fail("tests/c_host/liblds_poison.so missing: run __graft_entry__.build()")
+    helper = ctypes.CDLL(so)
+    helper.lds_poison.argtypes = [ctypes.c_float, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+    sink = torch.zeros(1, device="cuda")
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    for mode in ("analyser", "offline"):
+        pipe = _pipe((39, 64, 32, 16, 3), mode)
+        for F in (6, 9, 12, 21, 40, 70):
+            for seed in range(3):
+                rng = np.random.default_rng(100 * F + seed)
+                clip = rng.standard_normal(O.samples_for_frames(F)).astype(np.float32)
+                a = torch.from_numpy(clip).cuda()
+                want = pipe.labels(a)
+                assert helper.lds_poison(1e30, ctypes.c_void_p(sink.data_ptr()), 4 * n_cu, stream) == 0
+                got = pipe.labels(a, fused=True)
+                assert torch.equal(got, want), (mode, F, seed, got.tolist(), want.tolist())
+    assert sink.item() == 0.0  # the poison kernel saw its own LDS stores
+
+
 def test_fused_refuses_what_it_does_not_cover(torch_cuda):
     """Unaligned audio (a view one sample in) and a 40-filter plan do not
     qualify for the fused kernel: VadError without a workspace, and the

@@ -90,8 +90,9 @@ C_HOST_DIR = os.path.join(os.path.dirname(HERE), "tests", "c_host")
 
 def build_c_host(verbose=True):
     """The plain-C test host (tests/c_host): gcc against include/vad_amd.h and
-    the in-tree library, built here so GPU runs only execute it."""
-    cmd = ["make", "-C", C_HOST_DIR, "-s", "capi_host"]
+    the in-tree library, built here so GPU runs only execute it; and the
+    test-only LDS-poisoning helper (liblds_poison.so)."""
+    cmd = ["make", "-C", C_HOST_DIR, "-s", "capi_host", "liblds_poison.so"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

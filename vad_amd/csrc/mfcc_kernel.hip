@@ -1001,7 +1001,14 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_ffn_kernel(const MfccDev* __
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (wave + kDctGroups * i < MN) M[(4 + lane) * MN + wave + kDctGroups * i] = acc[i];
-    if (wave == 0 && lane < 4 * MN) M[lane] = ring[((tt + 1) & 1) * kRingFloats + kTile * MN + lane];
+    // rows 0..3: the previous tile's last four.  Tile 0 has none: its rows
+    // 0..3 feed only windows before wb (never stored), but they share wave
+    // 0's 16-window tile with stored windows, so they must hold finite,
+    // in-range values -- uninitialised LDS could force the tile's f16 rescale
+    // (layer_scale) and perturb its real windows (found by
+    // tests/test_gpu_fuzz.py: a fused label differing from the two-kernel one)
+    if (wave == 0 && lane < 4 * MN)
+      M[lane] = tt > 0 ? ring[((tt + 1) & 1) * kRingFloats + kTile * MN + lane] : 0.f;
   };
   // windows 16 wave .. 16 wave + 15 of ring buffer tt & 1 (row r = frame
   // fs + 64 tt - 4 + r; window 16 wave + jw starts at that row)
