@@ -95,3 +95,22 @@ def test_hop_rows_disjoint_accepts_contiguous_orderings(S, K, hl, pad):
     row = hl + pad
     assert hop_rows_disjoint(S, K, S * row, row, hl)   # (K, S, row): hop-major
     assert hop_rows_disjoint(S, K, row, K * row, hl)   # (S, K * row): stream-major
+
+
+@settings(FUZZ, max_examples=300)
+@given(words=st.lists(st.integers(0, 2 ** 32 - 1), min_size=1, max_size=3 * 39),
+       label=st.sampled_from([0, 1, 2]), n_cols=st.sampled_from([1, 3, 39]))
+def test_csv_formatter_any_float32(words, label, n_cols):
+    """vad_format_csv_rows (the native write_features formatter) against
+    csv.writer over numpy's float32 str, on arbitrary float32 bit patterns:
+    every exponent, subnormals, signed zeros, infinities and NaN payloads."""
+    import csv
+    import io
+    from vad_amd import dataset as D
+    k = len(words) // n_cols * n_cols
+    if k == 0:
+        return
+    rows = np.asarray(words[:k], np.uint32).view(np.float32).reshape(-1, n_cols)
+    s = io.StringIO()
+    csv.writer(s).writerows([list(r) + [np.float64(label)] for r in rows])
+    assert D.format_csv_rows(rows, label) == s.getvalue()
