@@ -261,7 +261,9 @@ int64_t vad_format_csv_rows(const float* rows, int64_t n_rows, int32_t n_cols, d
  *   2  np.std(|fft|) over all fft_len bins (:203-208)
  *   3+b stEnergy(|fft|[b*band_bins : (b+1)*band_bins])   (:171-197)
  * |fft| = |DFT_fft_len([zeros(pad), frame, zeros(pad)])| with
- * fft_len = frame_len + 2*pad (<= 1024) (:386-400; pad 0: the frame itself).
+ * fft_len = frame_len + 2*pad (:386-400; pad 0: the frame itself): frames of
+ * up to 8192 samples, fft_len up to 8193 (a power of two runs a radix-2 FFT,
+ * any other length -- the reference's odd pads -- a direct DFT).
  * stEnergy / stZCR are pyAudioAnalysis's (restated; the package is absent).
  * Frames are frames + f*frame_stride (fp32 samples, exact for int16 audio).
  * ------------------------------------------------------------------------- */

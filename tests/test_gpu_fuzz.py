@@ -161,3 +161,104 @@ def test_fuzz_stream_batch(torch_cuda, nets, S, T, K, log_amp, seed, kernel, gra
         x = pipe.features(a).cpu().numpy()
         ok = O.ffn_margin(x, lay) > MARGIN_TOL
         np.testing.assert_array_equal(got[s, 5:][ok], want[ok])
+
+
+@settings(FUZZ, max_examples=40)
+@given(depth=st.integers(1, 40), n_feat=st.sampled_from([13, 39]), n_classes=st.integers(2, 4),
+       seed=st.integers(0, 2 ** 32 - 1), nan_frac=st.sampled_from([0.0, 0.05]),
+       log_scale=st.floats(-4.0, 6.0))
+def test_fuzz_decision_tree(torch_cuda, depth, n_feat, n_classes, seed, nan_frac, log_scale):
+    """Fitted sklearn trees of random depth, width, class count and feature
+    scale, trained with missing values or without: the GPU walk
+    (tree_kernel.hip, thresholds rounded down to float) predicts what
+    sklearn's own predict does, on fresh float32 rows with NaNs, values
+    placed exactly on thresholds and their float neighbours."""
+    from sklearn.tree import DecisionTreeClassifier
+    from vad_amd.tree import TreeClassifier
+    rng = np.random.default_rng(seed)
+    scale = 10.0 ** (log_scale + rng.uniform(-1, 1, n_feat))
+    X = (rng.standard_normal((3000, n_feat)) * scale).astype(np.float32)
+    y = (X[:, 0] > 0).astype(int) + (X[:, 1 % n_feat] > scale[1 % n_feat]).astype(int)
+    y = (y + rng.integers(0, 2, len(y))) % n_classes
+    X[rng.random(X.shape) < nan_frac] = np.nan
+    clf = DecisionTreeClassifier(max_depth=depth, random_state=int(seed % 1000)).fit(X, y)
+    tree = TreeClassifier.from_sklearn(clf)
+    Xt = (rng.standard_normal((4000, n_feat)) * scale).astype(np.float32)
+    Xt[rng.random(Xt.shape) < 0.03] = np.nan
+    t = clf.tree_
+    # (a split that only separates missing values has an infinite threshold)
+    inner = np.nonzero((t.children_left >= 0) & (np.abs(t.threshold) < 3e38))[0]
+    if len(inner):  # rows sitting exactly on thresholds (as float32) and one ulp either side
+        pick = rng.choice(inner, size=min(600, 3 * len(inner)))
+        r = rng.integers(0, len(Xt), len(pick))
+        thr = t.threshold[pick].astype(np.float32)
+        delta = rng.integers(-1, 2, len(pick))
+        toward = np.where(delta < 0, -np.inf, np.inf).astype(np.float32)
+        Xt[r, t.feature[pick]] = np.where(delta == 0, thr, np.nextafter(thr, toward))
+    np.testing.assert_array_equal(tree.predict(Xt), clf.predict(Xt))
+
+
+def _spec_close(got, ref, tol=1e-5):
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    nr = np.linalg.norm(ref)
+    if nr == 0:
+        return np.abs(got).max() == 0
+    return np.linalg.norm(got - ref) / nr <= tol
+
+
+@settings(FUZZ, max_examples=80)
+@given(fft_n=st.one_of(st.integers(2, 8192), st.sampled_from([2, 3, 255, 256, 257, 511, 512, 513, 1024, 8192])),
+       len_frac=st.floats(0.01, 2.0), log_amp=st.floats(-3.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_spec_mag_any_length(torch_cuda, fft_n, len_frac, log_amp, seed):
+    """mfcc.get_spec_mag (mfcc.py:59-61) for every FFT length the reference
+    accepts (2..8192; zero-padded and truncated frames): the radix-16 kernels
+    at 512, a direct fp64 DFT otherwise, vs the oracle's float32 numpy FFT
+    within the spectrum tolerance (1e-5 of the frame's norm)."""
+    from vad_amd import mfcc as M
+    rng = np.random.default_rng(seed)
+    L = max(1, min(8192, int(round(len_frac * fft_n))))
+    frame = (rng.standard_normal(L) * 10.0 ** log_amp).astype(np.float32)
+    got = M.get_spec_mag(frame, fft_n)
+    ref = O.get_spec_mag(frame, fft_n)
+    assert got.shape == ref.shape == (fft_n // 2,)
+    assert _spec_close(got, ref), (fft_n, L)
+
+
+@settings(FUZZ, max_examples=60)
+@given(n=st.integers(0, 50_000), rows=st.integers(1, 4), coeff=st.floats(0.0, 1.0, exclude_max=True),
+       log_amp=st.floats(-3.0, 30.0), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_preemphasis(torch_cuda, n, rows, coeff, log_amp, seed):
+    """The optional pre-emphasis stage: bit-exact to the oracle's float32
+    numpy form (a rounded product, then the difference) for any length,
+    coefficient and magnitude, on a clip and on each row of a frame matrix."""
+    import torch
+    from vad_amd.plan import preemphasis
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal((rows, n)) * 10.0 ** log_amp).astype(np.float32)
+    t = torch.from_numpy(np.resize(x, (rows, max(n, 1)))).cuda()[:, :n].contiguous()
+    y2 = preemphasis(t, coeff).cpu().numpy()
+    y1 = preemphasis(t[0].contiguous(), coeff).cpu().numpy()
+    ref = np.stack([O.preemphasis(r, coeff) for r in x]) if n else np.zeros((rows, 0), np.float32)
+    np.testing.assert_array_equal(y1.view(np.uint32), ref[0].view(np.uint32))
+    np.testing.assert_array_equal(y2.view(np.uint32), ref.view(np.uint32))
+
+
+@settings(FUZZ, max_examples=40)
+@given(frame_size=st.one_of(st.integers(64, 1600), st.integers(1601, 8192), st.sampled_from([513, 1025, 4097, 8192])),
+       rate=st.sampled_from([8000, 16000, 22050, 44100]),
+       log_amp=st.floats(-3.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_simple_features(torch_cuda, frame_size, rate, log_amp, seed):
+    """SimpleAnalyser's per-frame features (simple_analyzer.py:162-215, fp64
+    on the GPU) for frame sizes up to 8192 samples -- FFT lengths a power of
+    two (radix-2 per wave) or one more (the reference's odd pads: a direct
+    DFT) -- and any rate, vs the oracle, relative 1e-9."""
+    from vad_amd.simple_analyser import SimpleAnalyser
+    rng = np.random.default_rng(seed)
+    sa = SimpleAnalyser(rate, frame_size, 5)
+    fr = rng.standard_normal((24, frame_size)) * 10.0 ** log_amp
+    fr[3] = 0.0  # a silent frame
+    got = sa.frame_features(fr)
+    ref = np.stack([O.simple_frame_features(f.astype(np.float32).astype(np.float64), frame_size, rate,
+                                            sa.spectral_bands) for f in fr])
+    np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())

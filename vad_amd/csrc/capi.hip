@@ -703,7 +703,7 @@ int vad_simple_features(const float* frames, int64_t n_frames, int32_t frame_len
                         int32_t n_bands, double* out, void* stream) {
   if (n_frames < 0 || frame_len < 2 || pad < 0 || frame_stride < 0 || band_bins < 1 || n_bands < 0)
     return VAD_EINVAL;
-  if (fft_len != frame_len + 2 * pad || fft_len > 1024 || n_bands * band_bins > fft_len)
+  if (fft_len != frame_len + 2 * pad || frame_len > 8192 || fft_len > 8193 || n_bands * band_bins > fft_len)
     return VAD_EUNSUPPORTED;
   if (n_frames == 0) return VAD_OK;
   if (!frames || !out) return VAD_EINVAL;

@@ -14,13 +14,15 @@
 //
 // Power-of-two L (the reference's 400-sample frames: L = 512): one wave per
 // frame (simple_features_wave_kernel, below); otherwise (e.g. 401 samples:
-// L = 513) one 256-thread workgroup per frame with a direct DFT.
+// L = 513) one 256-thread workgroup per frame with a direct DFT.  Frames of
+// up to 8192 samples: L <= 8192, or 8193 when the pad is odd.
 #include "vad_common.h"
 
 namespace vad {
 
 constexpr int kSimpleThreads = 256;
-constexpr int kSimpleMaxL = 1024;
+constexpr int kSimpleMaxL = 8193;
+constexpr int kSimpleLds = 160 * 1024;
 
 // Workgroup sum: a butterfly within each wave (DPP / permute shuffles),
 // then the four wave partials in a fixed order (deterministic).
@@ -37,10 +39,13 @@ __device__ double block_sum(double v, double* red) {
 
 // Non-power-of-two L (e.g. 401 samples: L = 513): one workgroup per frame,
 // direct DFT (the power-of-two lengths go to simple_features_wave_kernel).
+// Dynamic LDS: the padded frame re[L], then the magnitudes mag[L].
 __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     const float* __restrict__ frames, int64_t n_frames, int frame_len, int64_t frame_stride,
     int L, int pad, int band_bins, int n_bands, double* __restrict__ out) {
-  __shared__ double re[kSimpleMaxL];
+  extern __shared__ double dsm[];
+  double* re = dsm;
+  double* mag = dsm + L;
   __shared__ double red[kSimpleThreads / 64];
   const int t = threadIdx.x;
   const int n_out = 3 + n_bands;
@@ -66,9 +71,7 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     }
     __syncthreads();
     double mag_sum = 0.0;
-    double mk[kSimpleMaxL / kSimpleThreads + 1];
-    int q = 0;
-    for (int k = t; k < L; k += kSimpleThreads, ++q) {
+    for (int k = t; k < L; k += kSimpleThreads) {
       double ar = 0.0, ai = 0.0;
       int kn = 0;
       for (int n = 0; n < L; ++n) {
@@ -79,26 +82,22 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
         kn += k;
         if (kn >= L) kn -= L;
       }
-      mk[q] = sqrt(ar * ar + ai * ai);
-    }
-    __syncthreads();
-    q = 0;
-    for (int k = t; k < L; k += kSimpleThreads, ++q) {
-      re[k] = mk[q];  // magnitudes
-      mag_sum += mk[q];
+      const double m = sqrt(ar * ar + ai * ai);
+      mag[k] = m;
+      mag_sum += m;
     }
     __syncthreads();
     const double mean = block_sum(mag_sum, red) / (double)L;
     double ssd = 0.0;
     for (int k = t; k < L; k += kSimpleThreads) {
-      const double d = re[k] - mean;
+      const double d = mag[k] - mean;
       ssd += d * d;
     }
     ssd = block_sum(ssd, red);
     double* o = out + f * n_out;
     for (int b = 0; b < n_bands; ++b) {
       double be = 0.0;
-      for (int k = b * band_bins + t; k < (b + 1) * band_bins; k += kSimpleThreads) be += re[k] * re[k];
+      for (int k = b * band_bins + t; k < (b + 1) * band_bins; k += kSimpleThreads) be += mag[k] * mag[k];
       be = block_sum(be, red);
       if (t == 0) o[3 + b] = be / (double)band_bins;
     }
@@ -126,24 +125,29 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// tw_lds: the W_L^j table in LDS (L <= 4096); above, each butterfly computes
+// its twiddle (the 8192-point frame's two 64 KB arrays fill the LDS).
 __global__ __launch_bounds__(kSimpleThreads) void simple_features_wave_kernel(
     const float* __restrict__ frames, int64_t n_frames, int frame_len, int64_t frame_stride,
-    int L, int pad, int band_bins, int n_bands, double* __restrict__ out) {
-  extern __shared__ double sm[];  // [L/2] cos, [L/2] sin, then per wave [L] re, [L] im
+    int L, int pad, int band_bins, int n_bands, int tw_lds, double* __restrict__ out) {
+  extern __shared__ double sm[];  // [L/2] cos, [L/2] sin (tw_lds), then per wave [L] re, [L] im
   double* twc = sm;
   double* tws = sm + (L >> 1);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  double* re = sm + L + wave * 2 * L;
+  const int waves = blockDim.x >> 6;
+  double* re = sm + (tw_lds ? L : 0) + wave * 2 * L;
   double* im = re + L;
   int log2L = 0;
   while ((1 << log2L) < L) ++log2L;
-  for (int j = threadIdx.x; j < (L >> 1); j += kSimpleThreads)
-    sincospi(-2.0 * (double)j / (double)L, &tws[j], &twc[j]);
+  if (tw_lds) {
+    for (int j = threadIdx.x; j < (L >> 1); j += blockDim.x)
+      sincospi(-2.0 * (double)j / (double)L, &tws[j], &twc[j]);
+  }
   __syncthreads();
   const int n_out = 3 + n_bands;
-  const int64_t nw = (int64_t)gridDim.x * (kSimpleThreads / 64);
-  for (int64_t f = (int64_t)blockIdx.x * (kSimpleThreads / 64) + wave; f < n_frames; f += nw) {
+  const int64_t nw = (int64_t)gridDim.x * waves;
+  for (int64_t f = (int64_t)blockIdx.x * waves + wave; f < n_frames; f += nw) {
     const float* x = frames + f * frame_stride;
     double e = 0.0, z = 0.0;
     for (int i = lane; i < frame_len; i += 64) {
@@ -171,7 +175,13 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_wave_kernel(
         const int grp = b / half, k = b - grp * half;
         const int i0 = grp * len + k, i1 = i0 + half;
         const int tw = k * (L / len);
-        const double c = twc[tw], s = tws[tw];
+        double c, s;
+        if (tw_lds) {
+          c = twc[tw];
+          s = tws[tw];
+        } else {
+          sincospi(-2.0 * (double)tw / (double)L, &s, &c);
+        }
         const double xr = re[i1] * c - im[i1] * s, xi = re[i1] * s + im[i1] * c;
         const double ar = re[i0], ai = im[i0];
         re[i0] = ar + xr;
@@ -214,21 +224,33 @@ hipError_t launch_simple_features(const float* frames, int64_t n_frames, int fra
                                   int64_t frame_stride, int L, int pad, int band_bins, int n_bands,
                                   double* out, hipStream_t st) {
   if (n_frames <= 0) return hipSuccess;
+  if (L > kSimpleMaxL) return hipErrorInvalidValue;
   if ((L & (L - 1)) == 0) {
-    int64_t blocks = (n_frames + 3) / 4;
-    if (blocks > 2048) blocks = 2048;
-    const size_t smem = (size_t)(L + 4 * 2 * L) * sizeof(double);  // L = 1024: 72 KB
+    // waves per block: as many (up to 4) as the LDS holds beside the twiddle
+    // table (L = 512: 36 KB; 2048: 144 KB; 4096: one wave, 96 KB; 8192: one
+    // wave, 128 KB, twiddles computed per butterfly)
+    const int tw_lds = L <= 4096;
+    const size_t tw_bytes = tw_lds ? (size_t)L * sizeof(double) : 0;
+    const size_t wave_bytes = (size_t)2 * L * sizeof(double);
+    int waves = 4;
+    while (waves > 1 && tw_bytes + waves * wave_bytes > (size_t)kSimpleLds) --waves;
+    const size_t smem = tw_bytes + waves * wave_bytes;
+    if (smem > (size_t)kSimpleLds) return hipErrorInvalidValue;
     static std::atomic<unsigned long long> attr_done{0};
-    const hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simple_features_wave_kernel),
-                                        (int)((kSimpleMaxL + 8 * kSimpleMaxL) * sizeof(double)),
-                                        attr_done);
+    hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simple_features_wave_kernel), kSimpleLds, attr_done);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(simple_features_wave_kernel, dim3((int)blocks), dim3(kSimpleThreads), smem, st,
-                       frames, n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, out);
+    int64_t blocks = (n_frames + waves - 1) / waves;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(simple_features_wave_kernel, dim3((int)blocks), dim3(64 * waves), smem, st,
+                       frames, n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, tw_lds, out);
     return hipGetLastError();
   }
+  static std::atomic<unsigned long long> attr_done_d{0};
+  const size_t smem = (size_t)2 * L * sizeof(double);  // L = 8193: 128 KB
+  hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simple_features_kernel), kSimpleLds - 1024, attr_done_d);
+  if (e != hipSuccess) return e;
   int64_t blocks = n_frames < 4096 ? n_frames : 4096;
-  hipLaunchKernelGGL(simple_features_kernel, dim3((int)blocks), dim3(kSimpleThreads), 0, st, frames,
+  hipLaunchKernelGGL(simple_features_kernel, dim3((int)blocks), dim3(kSimpleThreads), smem, st, frames,
                      n_frames, frame_len, frame_stride, L, pad, band_bins, n_bands, out);
   return hipGetLastError();
 }
