@@ -262,3 +262,34 @@ def test_fuzz_simple_features(torch_cuda, frame_size, rate, log_amp, seed):
     ref = np.stack([O.simple_frame_features(f.astype(np.float32).astype(np.float64), frame_size, rate,
                                             sa.spectral_bands) for f in fr])
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())
+
+
+@settings(FUZZ, max_examples=60)
+@given(fft_n=st.one_of(st.just(512), st.integers(64, 4096)), n_filters=st.integers(2, 64),
+       mfcc_frac=st.floats(0.0, 1.0), low=st.floats(0.0, 1000.0), high_frac=st.floats(0.3, 1.0),
+       sr=st.sampled_from([8000, 16000, 22050]), len_frac=st.floats(0.2, 1.5),
+       log_amp=st.floats(-1.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_get_mfcc_any_bank(torch_cuda, fft_n, n_filters, mfcc_frac, low, high_frac, sr, len_frac,
+                                log_amp, seed):
+    """mfcc.get_mfcc (mfcc.py:67-78) with any finite mel bank the reference's
+    get_mel_filterbanks builds (2..64 filters, 1..16 coefficients, any band
+    and rate, FFT lengths 64..4096 and 512): the runtime-table or direct-DFT
+    kernels vs the oracle within the MFCC tolerance; get_mfcc_from_spec on
+    the oracle's own spectrum likewise."""
+    import warnings
+    from vad_amd import mfcc as M
+    high = low + high_frac * (sr / 2 - low)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        fb = O.get_mel_filterbanks(low, high, fft_n, n_filters, sr)
+    if not np.isfinite(fb).all() or (fb.sum(axis=1) == 0).any():
+        return  # a degenerate bank (NaN rows, or filters with no bins)
+    mfcc_n = 1 + int(mfcc_frac * (min(16, n_filters) - 1))
+    rng = np.random.default_rng(seed)
+    frame = (rng.standard_normal(max(1, int(len_frac * fft_n))) * 10.0 ** log_amp).astype(np.float32)
+    got = M.get_mfcc(frame, fft_n, fb, mfcc_n)
+    ref = O.get_mfcc(frame, fft_n, fb, mfcc_n)
+    assert got.shape == ref.shape == (mfcc_n,)
+    assert_mfcc_close(got[None], ref[None])
+    spec = O.get_spec_mag(frame, fft_n)
+    assert_mfcc_close(M.get_mfcc_from_spec(spec, fb, mfcc_n)[None], O.get_mfcc_from_spec(spec, fb, mfcc_n)[None])

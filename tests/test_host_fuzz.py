@@ -114,3 +114,21 @@ def test_csv_formatter_any_float32(words, label, n_cols):
     s = io.StringIO()
     csv.writer(s).writerows([list(r) + [np.float64(label)] for r in rows])
     assert D.format_csv_rows(rows, label) == s.getvalue()
+
+
+@settings(FUZZ, max_examples=300)
+@given(low=st.floats(0.0, 4000.0), span=st.floats(0.05, 1.0), fft_n=st.integers(2, 8192),
+       n_filters=st.integers(1, 64), sr=st.sampled_from([8000, 16000, 22050, 44100, 48000]))
+def test_mel_filterbanks_any_parameters(low, span, fft_n, n_filters, sr):
+    """vad_amd.mfcc.get_mel_filterbanks (the host side of a plan, mfcc.py:5-56)
+    equals the oracle's restatement bit for bit -- NaN where the reference
+    divides 0 by 0 -- for any band, FFT length, filter count and rate."""
+    import warnings
+    from vad_amd import mfcc as M
+    high = low + span * (sr / 2 - low)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        got = M.get_mel_filterbanks(low, high, fft_n, n_filters, sr)
+        ref = O.get_mel_filterbanks(low, high, fft_n, n_filters, sr)
+    assert got.shape == ref.shape == (n_filters, fft_n // 2)
+    np.testing.assert_array_equal(got, ref)
