@@ -132,3 +132,29 @@ def test_mel_filterbanks_any_parameters(low, span, fft_n, n_filters, sr):
         ref = O.get_mel_filterbanks(low, high, fft_n, n_filters, sr)
     assert got.shape == ref.shape == (n_filters, fft_n // 2)
     np.testing.assert_array_equal(got, ref)
+
+
+@settings(FUZZ, max_examples=150)
+@given(count=st.integers(0, 3000), width=st.integers(1, 4), channels=st.integers(1, 2),
+       rate=st.sampled_from([8000, 16000, 44100]), keep=st.floats(0.0, 1.0), seed=st.integers(0, 2 ** 32 - 1))
+def test_sph_read_round_trip(tmp_path_factory, count, width, channels, rate, keep, seed):
+    """dataset.sph_read (sph.py:33-64) on SPHERE files written here: nine
+    header lines, then big-endian samples of any width; each sample is the
+    low 16 bits of its big-endian value (the reference's int16 store), a
+    truncated file leaves the missing samples 0."""
+    from vad_amd import dataset as D
+    rng = np.random.default_rng(seed)
+    vals = [int(v) for v in rng.integers(0, 256 ** width, count, dtype=np.uint64)]
+    header = [b"NIST_1A", b"   1024", b"sample_count -i %d" % count, b"sample_n_bytes -i %d" % width,
+              b"channel_count -i %d" % channels, b"sample_byte_format -s2 10",
+              b"sample_rate -i %d" % rate, b"sample_coding -s3 pcm", b"end_head"]
+    body = b"".join(v.to_bytes(width, "big") for v in vals)
+    cut = int(keep * len(body))
+    p = tmp_path_factory.mktemp("sph") / "a.sph"
+    p.write_bytes(b"\n".join(header) + b"\n" + body[:cut])
+    s = D.sph_read(str(p))
+    n_full = cut // width
+    want = np.zeros(count, np.int16)
+    want[:n_full] = np.array([v & 0xFFFF for v in vals[:n_full]], np.uint16).view(np.int16)
+    assert (s.channels, s.framerate, s.sample_width) == (channels, rate, width)
+    np.testing.assert_array_equal(s.data, want)
