@@ -293,3 +293,98 @@ def test_fuzz_get_mfcc_any_bank(torch_cuda, fft_n, n_filters, mfcc_frac, low, hi
     assert_mfcc_close(got[None], ref[None])
     spec = O.get_spec_mag(frame, fft_n)
     assert_mfcc_close(M.get_mfcc_from_spec(spec, fb, mfcc_n)[None], O.get_mfcc_from_spec(spec, fb, mfcc_n)[None])
+
+
+class _MarginRecorder:
+    """Oracle-side classifier: the fp64 forward's label, recording its top-2
+    margin per call (a label at a near-tie may legitimately differ)."""
+
+    def __init__(self, layers):
+        self.layers = layers
+        self.margins = []
+
+    def predict(self, x):
+        x = np.asarray(x, np.float64).reshape(1, -1)
+        self.margins.append(float(O.ffn_margin(x, self.layers)[0]))
+        return O.ffn_labels(x, self.layers)
+
+
+@settings(FUZZ, max_examples=30)
+@given(lens=st.lists(st.integers(1, 1500), min_size=6, max_size=40), log_amp=st.floats(0.0, 4.5),
+       seed=st.integers(0, 2 ** 32 - 1), foreign=st.booleans(), silent=st.booleans())
+def test_fuzz_analyser_drop_in(torch_cuda, nets, lens, log_amp, seed, foreign, silent):
+    """The drop-in SKLearnAnalyzer (sklearn_analyser.py:46-82) fed frames of
+    random lengths (the 512-point FFT zero-pads or truncates each), with the
+    FFN in its .npz form (the fused device step) or as a pickled foreign
+    classifier (device features, host predict): every call returns what the
+    reference class -- restated by the oracle's AnalyserOracle -- returns
+    (None, or the very frame object passed three calls earlier), wherever the
+    oracle's margin for that call is decisive."""
+    import pickle
+    import tempfile
+    from vad_amd.ffn import save_layers
+    from vad_amd.sklearn_analyser import SKLearnAnalyzer
+    lay = nets["ref39"]
+    rng = np.random.default_rng(seed)
+    frames = [(rng.standard_normal(n) * 10.0 ** log_amp).astype(np.float32) for n in lens]
+    if silent:
+        for i in rng.choice(len(frames), size=max(1, len(frames) // 4), replace=False):
+            frames[i][:] = 0.0
+    noise = [(rng.standard_normal(int(n)) * 10.0).astype(np.float32) for n in rng.integers(1, 800, 5)]
+    with tempfile.TemporaryDirectory() as d:
+        if foreign:
+            path = f"{d}/clf.pkl"
+            with open(path, "wb") as f:
+                pickle.dump(O.FFNPredictor(lay), f)
+        else:
+            path = f"{d}/ffn.npz"
+            save_layers(path, lay)
+        an = SKLearnAnalyzer(path)
+    rec = _MarginRecorder(lay)
+    ref = O.AnalyserOracle(rec)
+    for a in (an, ref):
+        a.load_init_inactive_frames(noise)
+    ids = {id(f): i for i, f in enumerate(frames)}
+    for i, fr in enumerate(frames):
+        got, want = an.feed_frame(fr), ref.feed_frame(fr)
+        g = None if got is None else ids[id(got)]
+        w = None if want is None else ids[id(want)]
+        if i < 5:
+            assert g is None and w is None
+        elif rec.margins[-1] > MARGIN_TOL:
+            assert g == w, (i, g, w, rec.margins[-1])
+
+
+@settings(FUZZ, max_examples=40)
+@given(n=st.integers(1, 200_000), c=st.integers(1, 16), log_scale=st.tuples(*[st.floats(-6, 6)] * 3),
+       offset=st.tuples(*[st.floats(-1e4, 1e4)] * 3), const_group=st.sampled_from([None, 0, 1, 2]),
+       seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_scale_features(torch_cuda, n, c, log_scale, offset, const_group, seed):
+    """scale_features (dataset/utils.py:5-34) on the device: one mean and one
+    population std per group (mfcc, delta1, delta2) over every value, two
+    passes in fp64 like np.std, then (x - mean) / std -- vs numpy in fp64 on
+    the same float32 rows, any row count, width, scale and offset (a mean
+    far from 0 with a small spread stresses the variance), a constant group
+    giving numpy's inf / nan."""
+    import torch
+    from vad_amd import dataset as D
+    rng = np.random.default_rng(seed)
+    x = np.empty((n, 3, c), np.float32)
+    for g in range(3):
+        x[:, g] = (offset[g] + rng.standard_normal((n, c)) * 10.0 ** log_scale[g]).astype(np.float32)
+    if const_group is not None:
+        x[:, const_group] = np.float32(offset[const_group])
+    t = torch.from_numpy(x.reshape(n, 3 * c).copy()).cuda()
+    mean, std = D.scale_rows_device(t)
+    a64 = x.astype(np.float64)
+    m_ref = a64.mean(axis=(0, 2))
+    s_ref = a64.std(axis=(0, 2))
+    np.testing.assert_allclose(mean, m_ref, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(std, s_ref, rtol=1e-9, atol=1e-12 * np.abs(m_ref).max())
+    got = t.cpu().numpy().reshape(n, 3, c)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ref = ((a64 - mean[None, :, None]) / std[None, :, None]).astype(np.float32)
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    np.testing.assert_array_equal(np.isinf(got), np.isinf(ref))
+    fin = np.isfinite(ref)
+    np.testing.assert_allclose(got[fin], ref[fin], rtol=3e-7, atol=3e-7 * max(1.0, np.abs(ref[fin]).max(initial=0)))
