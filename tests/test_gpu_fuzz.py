@@ -388,3 +388,75 @@ def test_fuzz_scale_features(torch_cuda, n, c, log_scale, offset, const_group, s
     np.testing.assert_array_equal(np.isinf(got), np.isinf(ref))
     fin = np.isfinite(ref)
     np.testing.assert_allclose(got[fin], ref[fin], rtol=3e-7, atol=3e-7 * max(1.0, np.abs(ref[fin]).max(initial=0)))
+
+
+@settings(FUZZ, max_examples=60)
+@given(frame_len=st.one_of(st.integers(1, 1200), st.sampled_from([400, 512, 513, 800])),
+       stride=st.one_of(st.integers(1, 1500), st.sampled_from([160, 400, 512])), n=st.integers(1, 300),
+       nf=st.sampled_from([26, 40, 33]), fft_n=st.sampled_from([512, 512, 1024, 300]),
+       log_amp=st.floats(-1.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_frame_matrix_mfcc(torch_cuda, frame_len, stride, n, nf, fft_n, log_amp, seed):
+    """vad_mfcc_f32 / _i16 and vad_spec_f32 over any framing of a buffer --
+    frame length 1..1200 (the FFT zero-pads or truncates), any stride
+    (overlapping, abutting or with gaps), any frame count -- on the compiled
+    26 / 40-filter kernels, the runtime-table kernel (33 filters) and the
+    direct DFT (other FFT lengths): every frame vs the oracle; int16 input
+    bit-identical to the same integer samples as fp32."""
+    import torch
+    from vad_amd.plan import MfccPlan
+    rng = np.random.default_rng(seed)
+    total = stride * (n - 1) + frame_len
+    buf = np.clip(np.rint(rng.standard_normal(total) * 10.0 ** log_amp), -32767, 32767).astype(np.float32)
+    fb = O.get_mel_filterbanks(300, 8000, fft_n, nf, 16000)
+    if not np.isfinite(fb).all():
+        return
+    plan = MfccPlan(fb, 13, fft_n)
+    a = torch.from_numpy(buf).cuda()
+    got = plan.mfcc(a, frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
+    frames = np.stack([buf[i * stride:i * stride + frame_len] for i in range(n)])
+    ref = np.stack([O.get_mfcc(f, fft_n, fb, 13) for f in frames])
+    assert_mfcc_close(got, ref)
+    got16 = plan.mfcc(a.to(torch.int16), frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
+    np.testing.assert_array_equal(got16, got)
+    spec = plan.spec(a, frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
+    for i in range(n):
+        assert _spec_close(spec[i], O.get_spec_mag(frames[i], fft_n)), i
+
+
+@settings(FUZZ, max_examples=30)
+@given(frame_size=st.integers(100, 1024), hop_frac=st.floats(0.02, 1.0), nf=st.sampled_from([26, 40]),
+       S=st.integers(1, 20), T=st.integers(6, 30), kernel=st.sampled_from(["hop", "three"]),
+       seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_stream_configs(torch_cuda, nets, frame_size, hop_frac, nf, S, T, kernel, seed):
+    """StreamBatch under any framing (frame 100..1024 samples, hop 2..100 %
+    of it) and either reference bank: each stream's labels equal the clip
+    path's (VadPipeline with the same MfccConfig) on that stream's samples,
+    wherever the oracle's margin on the clip path's device features is
+    decisive."""
+    import torch
+    from vad_amd.config import MfccConfig
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.stream import StreamBatch
+    hop = max(1, int(hop_frac * frame_size))
+    cfg = MfccConfig(frame_size=frame_size, hop=hop, n_filters=nf)
+    lay = nets["ref39"]
+    clf = FFNClassifier(lay)
+    rng = np.random.default_rng(seed)
+    n = hop * (T - 1) + frame_size + 1  # T frames under the strict '>' rule
+    clips = np.clip(np.rint(rng.standard_normal((S, n)) * 10.0 ** rng.uniform(0, 4, (S, 1))),
+                    -32767, 32767).astype(np.float32)
+    keep = frame_size - hop
+    sb = StreamBatch(S, clf, cfg=cfg, kernel=kernel)
+    sb.prime(torch.from_numpy(np.ascontiguousarray(clips[:, :keep])).cuda())
+    got = np.stack([sb.step(torch.from_numpy(np.ascontiguousarray(
+        clips[:, keep + hop * t: keep + hop * (t + 1)])).cuda()).cpu().numpy().copy() for t in range(T)], axis=1)
+    assert (got[:, :5] == 255).all()
+    pipe = VadPipeline(clf, cfg=cfg)
+    for s in range(S):
+        a = torch.from_numpy(clips[s]).cuda()
+        want = pipe.labels(a).cpu().numpy()
+        assert want.shape == (T - 5,)
+        x = pipe.features(a).cpu().numpy()
+        ok = O.ffn_margin(x, lay) > MARGIN_TOL
+        np.testing.assert_array_equal(got[s, 5:][ok], want[ok])
