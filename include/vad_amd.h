@@ -65,6 +65,9 @@ int64_t vad_n_frames(int64_t n_samples, int32_t frame_size, int32_t hop);
  * ------------------------------------------------------------------------- */
 int vad_mfcc_plan_create(const double* filterbank_host, int32_t n_filters, int32_t fft_n,
                          int32_t mfcc_n, int32_t lifter_L, vad_mfcc_plan** out);
+/* destroy: frees the plan's device tables with hipFree, which waits for the
+ * device, so launches still queued with the plan complete first (a plan
+ * captured in a hipGraph must outlive the graph's replays). */
 int vad_mfcc_plan_destroy(vad_mfcc_plan* plan);
 
 /* Kernel variant a plan dispatches to: 0 = runtime filterbank tables,

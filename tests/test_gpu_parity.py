@@ -1155,3 +1155,33 @@ def test_feature_range_edges(torch_cuda):
     lo = (base * np.float32(2.0 ** -90)).astype(np.float32)
     got = window_features(torch.from_numpy(lo).cuda()).cpu().numpy()
     assert np.isinf(got[:, :13]).all()  # squares underflow: var 0, e2 / 0
+
+
+def test_plan_destroy_waits_for_pending_work(torch_cuda):
+    """A plan collected while its kernels are still queued (the Python object
+    dropped right after an asynchronous launch on a side stream): destroy
+    frees the plan's device tables with hipFree, which waits for the device,
+    so the queued launches still read live tables -- labels and MFCCs equal
+    a run whose plans stay alive."""
+    import gc
+    import torch
+    from vad_amd.ffn import TOPOLOGY_BL13, FFNClassifier, random_layers
+    from vad_amd.plan import MfccPlan
+    F = 400_000
+    clip = torch.from_numpy(O.synth_clip(O.samples_for_frames(F), seed=41)).cuda()
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    lay = random_layers(TOPOLOGY_BL13, seed=3)
+    keep_p, keep_c = MfccPlan(fb), FFNClassifier(lay)
+    m_ref = keep_p.clip_mfcc(clip)
+    lab_ref = keep_c.plan.window_labels(m_ref)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        m = torch.empty_like(m_ref)
+        lab = torch.empty_like(lab_ref)
+        for _ in range(3):  # a queue of work behind the launches that use the plans
+            MfccPlan(fb).clip_mfcc(clip, out=m, stream=side)
+            FFNClassifier(lay).plan.window_labels(m, out=lab, stream=side)
+            gc.collect()  # the plans above are unreferenced now
+    side.synchronize()
+    assert torch.equal(m, m_ref) and torch.equal(lab, lab_ref)
