@@ -460,3 +460,60 @@ def test_fuzz_stream_configs(torch_cuda, nets, frame_size, hop_frac, nf, S, T, k
         x = pipe.features(a).cpu().numpy()
         ok = O.ffn_margin(x, lay) > MARGIN_TOL
         np.testing.assert_array_equal(got[s, 5:][ok], want[ok])
+
+
+@settings(FUZZ, max_examples=50)
+@given(dims=st.lists(st.integers(1, 64), min_size=2, max_size=5).map(lambda d: d[:-1] + [min(4, max(2, d[-1] % 5))]),
+       arith=st.sampled_from(["split_f16", "f32"]), log_scale=st.floats(-2.0, 2.0),
+       nan_rows=st.booleans(), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_ffn_any_topology(torch_cuda, dims, arith, log_scale, nan_rows, seed):
+    """FFNClassifier.predict (vad_ffn_predict) for any topology the build
+    takes (1..4 layers, widths up to 64, 2..4 classes): the specialised
+    split-f16 shapes where they apply, the padded exact-f32 kernel
+    otherwise; rows of any scale, some NaN (class 0, np.argmax's rule):
+    labels equal the fp64 oracle's wherever its top-2 margin exceeds 1e-4 of
+    the logit scale."""
+    from vad_amd.ffn import FFNClassifier, random_layers
+    rng = np.random.default_rng(seed)
+    lay = random_layers(tuple(dims), seed=int(seed % 1000))
+    try:
+        clf = FFNClassifier(lay, arith=arith)
+        clf.plan
+    except ValueError:
+        assert arith == "split_f16"  # split-f16 exists for the specialised shapes only
+        return
+    x = (rng.standard_normal((3000, dims[0])) * 10.0 ** log_scale).astype(np.float32)
+    if nan_rows:
+        x[rng.random(len(x)) < 0.05, rng.integers(0, dims[0])] = np.nan
+    got = clf.predict(x)
+    ref = O.ffn_labels(x, lay)
+    z, _ = O.ffn_forward(x, lay)
+    scale = np.nanmax(np.abs(z)) if np.isfinite(z).any() else 1.0
+    ok = O.ffn_margin(x, lay) > 1e-4 * max(scale, 1.0)
+    np.testing.assert_array_equal(got[ok], ref[ok])
+    assert ok.mean() > 0.95
+
+
+@settings(FUZZ, max_examples=30)
+@given(depth=st.integers(1, 30), offline=st.booleans(), F=st.integers(6, 3000),
+       seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_tree_windows(torch_cuda, depth, offline, F, seed):
+    """vad_features_tree (the tree over every 5-frame window, features
+    computed in the kernel): labels equal sklearn's predict on the device's
+    own window features (vad_features_f32), analyser (NaN windows included)
+    or offline form, for trees fitted on such features."""
+    import torch
+    from sklearn.tree import DecisionTreeClassifier
+    from vad_amd import _lib
+    from vad_amd import plan as P
+    from vad_amd.tree import TreeClassifier
+    rng = np.random.default_rng(seed)
+    clip = O.synth_clip(O.samples_for_frames(F), seed=int(seed % 10_000))
+    m = P.MfccPlan(O.get_mel_filterbanks(300, 8000, 512, 26, 16000)).clip_mfcc(torch.from_numpy(clip).cuda())
+    mode = _lib.FEAT_OFFLINE if offline else _lib.FEAT_ANALYSER
+    x = P.window_features(m, mode).cpu().numpy()
+    y = rng.integers(0, 2, len(x)) ^ (np.nan_to_num(x[:, 0]) > np.nanmedian(x[:, 0])).astype(int)
+    clf = DecisionTreeClassifier(max_depth=depth, random_state=0).fit(x, y)
+    tree = TreeClassifier.from_sklearn(clf)
+    got = tree.window_labels(m, mode).cpu().numpy()
+    np.testing.assert_array_equal(tree.classes_[got.astype(np.int64)], clf.predict(x))
