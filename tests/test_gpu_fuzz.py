@@ -517,3 +517,65 @@ def test_fuzz_tree_windows(torch_cuda, depth, offline, F, seed):
     tree = TreeClassifier.from_sklearn(clf)
     got = tree.window_labels(m, mode).cpu().numpy()
     np.testing.assert_array_equal(tree.classes_[got.astype(np.int64)], clf.predict(x))
+
+
+@settings(FUZZ, max_examples=50)
+@given(L=st.integers(1, 1024), h_frac=st.floats(0.0, 1.0), S=st.integers(1, 300), fpad=st.integers(0, 70),
+       hpad=st.integers(0, 70), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_stream_push_hop(torch_cuda, L, h_frac, S, fpad, hpad, seed):
+    """vad_stream_push_hop (the three-kernel form's frame assembly) for any
+    frame length 1..1024, hop 1..L, padded row strides and stream count:
+    every row shifted left by the hop with the new samples appended, the
+    padding columns untouched."""
+    import torch
+    from vad_amd import _lib
+    H = max(1, int(round(h_frac * L)))
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    frames = torch.randn((S, L + fpad), device="cuda", generator=g)
+    hop = torch.randn((S, H + hpad), device="cuda", generator=g)
+    want = frames.clone()
+    want[:, :L] = torch.cat([frames[:, H:L], hop[:, :H]], dim=1)
+    _lib.check(_lib.lib().vad_stream_push_hop(_lib.ptr(frames), L + fpad, L, _lib.ptr(hop), H + hpad, H, S,
+                                              _lib.stream_ptr()), "vad_stream_push_hop")
+    torch.cuda.synchronize()
+    assert torch.equal(frames, want)
+
+
+@settings(FUZZ, max_examples=50)
+@given(F=st.integers(0, 400), n=st.integers(1, 16), offline=st.booleans(), flat_cols=st.integers(0, 3),
+       log_scale=st.floats(-6.0, 6.0), seed=st.integers(0, 2 ** 32 - 1))
+def test_fuzz_window_features_any_width(torch_cuda, F, n, offline, flat_cols, log_scale, seed):
+    """vad_features_f32 over MFCC rows of any width 1..16 (the plans' MFCC
+    counts) and any frame count (F - 5 windows, none below 6 frames), some
+    coefficients constant (the analyser's 0/0 -> NaN in Mn and D2): the
+    oracle's window features of the same fp32 rows, NaN positions exact,
+    values to fp32 rounding of the window statistics."""
+    import torch
+    from vad_amd import _lib
+    from vad_amd import plan as P
+    rng = np.random.default_rng(seed)
+    m = (rng.standard_normal((F, n)) * 10.0 ** log_scale).astype(np.float32)
+    for c in rng.choice(n, size=min(flat_cols, n) if F else 0, replace=False):
+        m[:, c] = m[0, c]
+    mode = _lib.FEAT_OFFLINE if offline else _lib.FEAT_ANALYSER
+    t = torch.from_numpy(np.resize(m, (max(F, 1), n))).cuda()[:F].contiguous()
+    got = P.window_features(t, mode).cpu().numpy().astype(np.float64)
+    rows = max(F - 5, 0)
+    assert got.shape == (rows, 3 * n)
+    if rows == 0:
+        return
+    ref = (O.offline_features(m).reshape(rows, 3 * n) if offline else O.analyser_features_fast(m))
+    np.testing.assert_array_equal(np.isnan(got), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    scale = np.abs(m).max()
+    if offline:  # differences of fp32 rows: exact up to one rounding
+        assert np.abs(got[ok] - ref[ok]).max() <= 4e-7 * scale
+    else:  # Mn divides by the window std: its rounding scales with |M| / std
+        win = np.stack([m[d:d + rows].astype(np.float64) for d in range(5)], axis=1)
+        std = win.std(axis=1)
+        mag = np.abs(win).max(axis=1)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            b_mn = 4e-6 * mag / std * (1 + np.abs(np.nan_to_num(ref[:, :n]))) + 1e-6
+        err = np.abs(got - ref)
+        b = np.concatenate([b_mn, 4e-7 * mag + 1e-30, 2 * b_mn + 1e-6 * mag], axis=1)
+        assert (err[ok] <= b[ok]).all(), float(np.max(err[ok] / b[ok]))
