@@ -406,6 +406,12 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   constexpr int NSD = kDiff ? TP::TIL * 4 + 1 : 0;
   constexpr int NSLP = (NSL + NSD + 3) & ~3;
   __shared__ __attribute__((aligned(16))) float slot_s[kLdsSlots ? 4 * NSLP : 1];
+#ifndef VAD_FFN_PRIO
+#define VAD_FFN_PRIO 3
+#endif
+#ifndef VAD_FFN_PRIO_FEAT
+#define VAD_FFN_PRIO_FEAT 0
+#endif
 #ifndef VAD_FFN_LO_ALL
 #define VAD_FFN_LO_ALL 1  // 1: every lo half in LDS; 0: those after layer 0 only
 #endif
@@ -498,7 +504,18 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     for (int q = 0; q < kWRowRegs; ++q)
       if (lane + 64 * q < kWRows) R[lane + 64 * q] = pre[q];
     load(tn < n_tiles ? tn : t, pre);
+#if VAD_FFN_PRIO_FEAT
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(VAD_FFN_PRIO_FEAT);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
+#if VAD_FFN_PRIO || VAD_FFN_PRIO_FEAT
+    // experiment: the MFMA / split chain at raised issue priority
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(VAD_FFN_PRIO);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     f32x4 z;
     int lab;
     if constexpr (kDiff) {
@@ -508,6 +525,11 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
       lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
                                wave_tile_in_bounded<MODE, IN>>(X, FL, lane, fh, fbs, fvs, net.n_classes, z);
     }
+#if VAD_FFN_PRIO && !VAD_FFN_PRIO_FEAT
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) {
       labels[w] = (uint8_t)lab;
