@@ -4,7 +4,8 @@ alternated: python tools/ab_ffn.py LIB_A LIB_B [...] [rounds]
 Per build and round: the 13-64-64-2 (and 39-64-32-16-3) window kernel on the
 MFCC rows of the C3 clip (1M frames), median of 7 batches of 20 launches after
 a 0.5 s warm-up; the labels of the last launch are saved and compared with the
-first build's (count of differing windows)."""
+first build's (count of differing windows).  AB_ARITH=f32 times the
+exact-f32 kernel instead of the split-f16 one."""
 import json
 import os
 import subprocess
@@ -24,7 +25,7 @@ a = synth_audio(160 * (F - 1) + 401, 1, dev)
 m = VadPipeline().mfcc(a)
 out = {}
 for name, topo in (("bl13", TOPOLOGY_BL13), ("ref39", TOPOLOGY_REF39)):
-    plan = FFNClassifier(random_layers(topo, seed=3)).plan
+    plan = FFNClassifier(random_layers(topo, seed=3), arith=os.environ.get("AB_ARITH", "split_f16")).plan
     lab = torch.empty((F - 5,), dtype=torch.uint8, device=dev)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.5:

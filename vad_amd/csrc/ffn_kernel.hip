@@ -78,6 +78,9 @@ __global__ __launch_bounds__(256) void ffn_kernel(FfnDev net, const float* __res
 //   C  each wave runs the MFMA chain on 16 windows with its layer-0 B
 //      operands read from the tile, then the argmax.
 // rows / X are double-buffered, so two barriers per chunk order the phases.
+#ifndef VAD_FFN_WIN_PRIO
+#define VAD_FFN_WIN_PRIO 1  // issue priority of phase C, the MFMA chain (0: none)
+#endif
 constexpr int kChunk = 64;
 constexpr int kXStride = 68;  // floats per feature row: 16-B aligned, conflict-free b128 reads
 
@@ -236,6 +239,13 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
     // ---- C: MFMA chain, 16 windows per wave --------------------------------
     const int wl = wv * 16 + jw;
     const int64_t w = base + wl;
+#if VAD_FFN_WIN_PRIO
+    // the MFMA chain at raised issue priority, as in ffn_wave_kernel (A/B,
+    // exact f32: 116.6 -> 114.4 us per 1M windows, profiles/r05/ab/ffn_win_prio_ab.json)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(VAD_FFN_WIN_PRIO);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     f32x4 z;
     if constexpr (H3) {
       // windows past nwin read stale (finite) features: computed, not stored
@@ -268,6 +278,11 @@ __device__ __forceinline__ void ffn_window_body(const FfnDev& net, const float* 
       }
       z = mlp_forward<KS0, T1, T2, T3, T4, NC>(fa, fb, fv, x);
     }
+#if VAD_FFN_WIN_PRIO
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
     if (g == 0 && wl < nwin) {
       labels[w] = (uint8_t)argmax_classes(z, net.n_classes);
       store_logits(net.logits, w, z, net.n_classes);
@@ -406,6 +421,11 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   constexpr int NSD = kDiff ? TP::TIL * 4 + 1 : 0;
   constexpr int NSLP = (NSL + NSD + 3) & ~3;
   __shared__ __attribute__((aligned(16))) float slot_s[kLdsSlots ? 4 * NSLP : 1];
+// issue priority of a tile's MFMA / split / label chain (VAD_FFN_PRIO) and of
+// its features (VAD_FFN_PRIO_FEAT; when set, held to the next tile's
+// features).  A/B (profiles/r05/ab/ffn_prio_ab_*.json): the chain at 3 takes
+// 13-64-64-2 from 50.2 to 48.5 us per 1M windows; features at 3 gain half
+// that, both raised no more
 #ifndef VAD_FFN_PRIO
 #define VAD_FFN_PRIO 3
 #endif
@@ -511,7 +531,8 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
 #endif
     wave_tile_features<IN, XS, MODE>(R, X, FL, lane);
 #if VAD_FFN_PRIO || VAD_FFN_PRIO_FEAT
-    // experiment: the MFMA / split chain at raised issue priority
+    // the MFMA / split chain at raised issue priority: the SIMD's arbiter
+    // favours the wave deepest in its chain over the others' features
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(VAD_FFN_PRIO);
     __builtin_amdgcn_sched_barrier(0);
