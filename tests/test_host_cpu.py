@@ -26,6 +26,14 @@ def test_library_exports_header_symbols():
     assert set(syms) == set(_lib.SIGNATURES), set(syms) ^ set(_lib.SIGNATURES)
 
 
+def test_integration_maps_every_header_symbol():
+    """INTEGRATION.md names every entry point the header declares (the map
+    from each one to the reference interface it replaces)."""
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    missing = [s for s in header_symbols() if not re.search(r"\b" + s + r"\b", doc)]
+    assert not missing, missing
+
+
 def test_library_is_gfx950():
     from vad_amd import _lib
     blob = open(_lib.LIB_PATH, "rb").read()
