@@ -22,8 +22,11 @@ the analyser or offline feature form and a fixture network, then checks:
                    wherever the margin is decisive
 
 derandomize=True: every run draws the same examples (no flaky GPU runs);
-database=None: nothing is written next to the tests.
+database=None: nothing is written next to the tests.  A deep run
+(VAD_FUZZ_SCALE=k, VAD_FUZZ_SEED=s) draws k times the examples from seed s
+instead -- a search for new defects, not part of the round-end suite.
 """
+import os
 import numpy as np
 import pytest
 
@@ -37,8 +40,17 @@ pytestmark = pytest.mark.gpu
 
 MFCC_TOL = 1e-4
 MARGIN_TOL = 0.05
-FUZZ = settings(max_examples=120, deadline=None, derandomize=True, database=None,
+_SCALE = int(os.environ.get("VAD_FUZZ_SCALE", "1"))
+_SEED = os.environ.get("VAD_FUZZ_SEED")
+FUZZ = settings(max_examples=120 * _SCALE, deadline=None, derandomize=_SEED is None, database=None,
                 suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+
+
+def fuzz(n):
+    """The suite's settings with n examples per test (times VAD_FUZZ_SCALE);
+    with VAD_FUZZ_SEED the examples come from that seed."""
+    s = settings(FUZZ, max_examples=n * _SCALE)
+    return s if _SEED is None else (lambda f: hyp.seed(int(_SEED))(s(f)))
 
 
 @pytest.fixture(scope="module")
@@ -79,7 +91,7 @@ def assert_mfcc_close(got, ref):
     assert mx.max() <= MFCC_TOL, (mx.max(), int(mx.argmax()))
 
 
-@FUZZ
+@fuzz(120)
 @given(n=st.one_of(st.integers(0, 30000), st.sampled_from([0, 399, 400, 401, 560, 561, 1200, 1201, 10481])),
        log_amp=st.floats(-2.0, 4.6), seed=st.integers(0, 2 ** 32 - 1),
        silence=st.one_of(st.none(), st.tuples(st.floats(0, 1), st.floats(0, 1))),
@@ -124,7 +136,7 @@ def test_fuzz_clip_path(torch_cuda, nets, n, log_amp, seed, silence, i16, offlin
     np.testing.assert_array_equal(lab[ok], O.ffn_labels(x, lay)[ok])
 
 
-@settings(FUZZ, max_examples=50)
+@fuzz(50)
 @given(S=st.integers(1, 70), T=st.integers(6, 40), K=st.sampled_from([1, 2, 3, 8]),
        log_amp=st.floats(-1.0, 4.6), seed=st.integers(0, 2 ** 32 - 1), kernel=st.sampled_from(["hop", "three"]),
        graph=st.booleans())
@@ -163,7 +175,7 @@ def test_fuzz_stream_batch(torch_cuda, nets, S, T, K, log_amp, seed, kernel, gra
         np.testing.assert_array_equal(got[s, 5:][ok], want[ok])
 
 
-@settings(FUZZ, max_examples=40)
+@fuzz(40)
 @given(depth=st.integers(1, 40), n_feat=st.sampled_from([13, 39]), n_classes=st.integers(2, 4),
        seed=st.integers(0, 2 ** 32 - 1), nan_frac=st.sampled_from([0.0, 0.05]),
        log_scale=st.floats(-4.0, 6.0))
@@ -207,7 +219,7 @@ def _spec_close(got, ref, tol=1e-5):
     return np.linalg.norm(got - ref) / nr <= tol
 
 
-@settings(FUZZ, max_examples=80)
+@fuzz(80)
 @given(fft_n=st.one_of(st.integers(2, 8192), st.sampled_from([2, 3, 255, 256, 257, 511, 512, 513, 1024, 8192])),
        len_frac=st.floats(0.01, 2.0), log_amp=st.floats(-3.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
 def test_fuzz_spec_mag_any_length(torch_cuda, fft_n, len_frac, log_amp, seed):
@@ -225,7 +237,7 @@ def test_fuzz_spec_mag_any_length(torch_cuda, fft_n, len_frac, log_amp, seed):
     assert _spec_close(got, ref), (fft_n, L)
 
 
-@settings(FUZZ, max_examples=60)
+@fuzz(60)
 @given(n=st.integers(0, 50_000), rows=st.integers(1, 4), coeff=st.floats(0.0, 1.0, exclude_max=True),
        log_amp=st.floats(-3.0, 30.0), seed=st.integers(0, 2 ** 32 - 1))
 def test_fuzz_preemphasis(torch_cuda, n, rows, coeff, log_amp, seed):
@@ -244,7 +256,7 @@ def test_fuzz_preemphasis(torch_cuda, n, rows, coeff, log_amp, seed):
     np.testing.assert_array_equal(y2.view(np.uint32), ref.view(np.uint32))
 
 
-@settings(FUZZ, max_examples=40)
+@fuzz(40)
 @given(frame_size=st.one_of(st.integers(64, 1600), st.integers(1601, 8192), st.sampled_from([513, 1025, 4097, 8192])),
        rate=st.sampled_from([8000, 16000, 22050, 44100]),
        log_amp=st.floats(-3.0, 4.5), seed=st.integers(0, 2 ** 32 - 1))
@@ -264,7 +276,7 @@ def test_fuzz_simple_features(torch_cuda, frame_size, rate, log_amp, seed):
     np.testing.assert_allclose(got, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())
 
 
-@settings(FUZZ, max_examples=60)
+@fuzz(60)
 @given(fft_n=st.one_of(st.just(512), st.integers(64, 4096)), n_filters=st.integers(2, 64),
        mfcc_frac=st.floats(0.0, 1.0), low=st.floats(0.0, 1000.0), high_frac=st.floats(0.3, 1.0),
        sr=st.sampled_from([8000, 16000, 22050]), len_frac=st.floats(0.2, 1.5),
@@ -309,7 +321,7 @@ class _MarginRecorder:
         return O.ffn_labels(x, self.layers)
 
 
-@settings(FUZZ, max_examples=30)
+@fuzz(30)
 @given(lens=st.lists(st.integers(1, 1500), min_size=6, max_size=40), log_amp=st.floats(0.0, 4.5),
        seed=st.integers(0, 2 ** 32 - 1), foreign=st.booleans(), silent=st.booleans())
 def test_fuzz_analyser_drop_in(torch_cuda, nets, lens, log_amp, seed, foreign, silent):
@@ -355,7 +367,7 @@ def test_fuzz_analyser_drop_in(torch_cuda, nets, lens, log_amp, seed, foreign, s
             assert g == w, (i, g, w, rec.margins[-1])
 
 
-@settings(FUZZ, max_examples=40)
+@fuzz(40)
 @given(n=st.integers(1, 200_000), c=st.integers(1, 16), log_scale=st.tuples(*[st.floats(-6, 6)] * 3),
        offset=st.tuples(*[st.floats(-1e4, 1e4)] * 3), const_group=st.sampled_from([None, 0, 1, 2]),
        seed=st.integers(0, 2 ** 32 - 1))
@@ -390,7 +402,7 @@ def test_fuzz_scale_features(torch_cuda, n, c, log_scale, offset, const_group, s
     np.testing.assert_allclose(got[fin], ref[fin], rtol=3e-7, atol=3e-7 * max(1.0, np.abs(ref[fin]).max(initial=0)))
 
 
-@settings(FUZZ, max_examples=60)
+@fuzz(60)
 @given(frame_len=st.one_of(st.integers(1, 1200), st.sampled_from([400, 512, 513, 800])),
        stride=st.one_of(st.integers(1, 1500), st.sampled_from([160, 400, 512])), n=st.integers(1, 300),
        nf=st.sampled_from([26, 40, 33]), fft_n=st.sampled_from([512, 512, 1024, 300]),
@@ -423,7 +435,7 @@ def test_fuzz_frame_matrix_mfcc(torch_cuda, frame_len, stride, n, nf, fft_n, log
         assert _spec_close(spec[i], O.get_spec_mag(frames[i], fft_n)), i
 
 
-@settings(FUZZ, max_examples=30)
+@fuzz(30)
 @given(frame_size=st.integers(100, 1024), hop_frac=st.floats(0.02, 1.0), nf=st.sampled_from([26, 40]),
        S=st.integers(1, 20), T=st.integers(6, 30), kernel=st.sampled_from(["hop", "three"]),
        seed=st.integers(0, 2 ** 32 - 1))
@@ -462,7 +474,7 @@ def test_fuzz_stream_configs(torch_cuda, nets, frame_size, hop_frac, nf, S, T, k
         np.testing.assert_array_equal(got[s, 5:][ok], want[ok])
 
 
-@settings(FUZZ, max_examples=50)
+@fuzz(50)
 @given(dims=st.lists(st.integers(1, 64), min_size=2, max_size=5).map(lambda d: d[:-1] + [min(4, max(2, d[-1] % 5))]),
        arith=st.sampled_from(["split_f16", "f32"]), log_scale=st.floats(-2.0, 2.0),
        nan_rows=st.booleans(), seed=st.integers(0, 2 ** 32 - 1))
@@ -494,7 +506,7 @@ def test_fuzz_ffn_any_topology(torch_cuda, dims, arith, log_scale, nan_rows, see
     assert ok.mean() > 0.95
 
 
-@settings(FUZZ, max_examples=30)
+@fuzz(30)
 @given(depth=st.integers(1, 30), offline=st.booleans(), F=st.integers(6, 3000),
        seed=st.integers(0, 2 ** 32 - 1))
 def test_fuzz_tree_windows(torch_cuda, depth, offline, F, seed):
@@ -519,7 +531,7 @@ def test_fuzz_tree_windows(torch_cuda, depth, offline, F, seed):
     np.testing.assert_array_equal(tree.classes_[got.astype(np.int64)], clf.predict(x))
 
 
-@settings(FUZZ, max_examples=50)
+@fuzz(50)
 @given(L=st.integers(1, 1024), h_frac=st.floats(0.0, 1.0), S=st.integers(1, 300), fpad=st.integers(0, 70),
        hpad=st.integers(0, 70), seed=st.integers(0, 2 ** 32 - 1))
 def test_fuzz_stream_push_hop(torch_cuda, L, h_frac, S, fpad, hpad, seed):
@@ -541,7 +553,7 @@ def test_fuzz_stream_push_hop(torch_cuda, L, h_frac, S, fpad, hpad, seed):
     assert torch.equal(frames, want)
 
 
-@settings(FUZZ, max_examples=50)
+@fuzz(50)
 @given(F=st.integers(0, 400), n=st.integers(1, 16), offline=st.booleans(), flat_cols=st.integers(0, 3),
        log_scale=st.floats(-6.0, 6.0), seed=st.integers(0, 2 ** 32 - 1))
 def test_fuzz_window_features_any_width(torch_cuda, F, n, offline, flat_cols, log_scale, seed):
