@@ -12,6 +12,8 @@
                  the C ABI requires first), and accepts both contiguous
                  orderings
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -21,10 +23,17 @@ hyp = pytest.importorskip("hypothesis")
 from hypothesis import given, settings  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
-FUZZ = settings(max_examples=200, deadline=None, derandomize=True, database=None)
+_SCALE = int(os.environ.get("VAD_FUZZ_SCALE", "1"))  # deep runs: see tests/test_gpu_fuzz.py
+_SEED = os.environ.get("VAD_FUZZ_SEED")
+FUZZ = settings(max_examples=200 * _SCALE, deadline=None, derandomize=_SEED is None, database=None)
 
 
-@FUZZ
+def fuzz(n):
+    s = settings(FUZZ, max_examples=n * _SCALE)
+    return s if _SEED is None else (lambda f: hyp.seed(int(_SEED))(s(f)))
+
+
+@fuzz(200)
 @given(n=st.integers(0, 2_000_000), world=st.integers(1, 8))
 def test_split_clip_partitions_windows(n, world):
     from vad_amd.dist import n_frames, split_clip
@@ -42,7 +51,7 @@ def test_split_clip_partitions_windows(n, world):
     assert nxt == n_win
 
 
-@settings(FUZZ, max_examples=25)
+@fuzz(25)
 @given(frames=st.integers(0, 60), extra=st.integers(0, 159), world=st.integers(1, 5),
        seed=st.integers(0, 2 ** 31))
 def test_split_clip_labels_concatenate(frames, extra, world, seed):
@@ -76,7 +85,7 @@ def _rows_disjoint_brute(S, K, block, hs, hl):
     return all(b - a >= hl for a, b in zip(starts, starts[1:]))
 
 
-@FUZZ
+@fuzz(200)
 @given(S=st.integers(1, 12), K=st.integers(1, 9), hl=st.integers(1, 200),
        block=st.integers(-3000, 3000), gap=st.integers(0, 3000))
 def test_hop_rows_disjoint_is_sound(S, K, block, gap, hl):
@@ -88,7 +97,7 @@ def test_hop_rows_disjoint_is_sound(S, K, block, gap, hl):
         assert _rows_disjoint_brute(S, K, block, hs, hl)
 
 
-@FUZZ
+@fuzz(200)
 @given(S=st.integers(1, 64), K=st.integers(1, 16), hl=st.integers(1, 400), pad=st.integers(0, 64))
 def test_hop_rows_disjoint_accepts_contiguous_orderings(S, K, hl, pad):
     from vad_amd.stream import hop_rows_disjoint
@@ -97,7 +106,7 @@ def test_hop_rows_disjoint_accepts_contiguous_orderings(S, K, hl, pad):
     assert hop_rows_disjoint(S, K, row, K * row, hl)   # (S, K * row): stream-major
 
 
-@settings(FUZZ, max_examples=300)
+@fuzz(300)
 @given(words=st.lists(st.integers(0, 2 ** 32 - 1), min_size=1, max_size=3 * 39),
        label=st.sampled_from([0, 1, 2]), n_cols=st.sampled_from([1, 3, 39]))
 def test_csv_formatter_any_float32(words, label, n_cols):
@@ -116,7 +125,7 @@ def test_csv_formatter_any_float32(words, label, n_cols):
     assert D.format_csv_rows(rows, label) == s.getvalue()
 
 
-@settings(FUZZ, max_examples=300)
+@fuzz(300)
 @given(low=st.floats(0.0, 4000.0), span=st.floats(0.05, 1.0), fft_n=st.integers(2, 8192),
        n_filters=st.integers(1, 64), sr=st.sampled_from([8000, 16000, 22050, 44100, 48000]))
 def test_mel_filterbanks_any_parameters(low, span, fft_n, n_filters, sr):
@@ -134,7 +143,7 @@ def test_mel_filterbanks_any_parameters(low, span, fft_n, n_filters, sr):
     np.testing.assert_array_equal(got, ref)
 
 
-@settings(FUZZ, max_examples=150)
+@fuzz(150)
 @given(count=st.integers(0, 3000), width=st.integers(1, 4), channels=st.integers(1, 2),
        rate=st.sampled_from([8000, 16000, 44100]), keep=st.floats(0.0, 1.0), seed=st.integers(0, 2 ** 32 - 1))
 def test_sph_read_round_trip(tmp_path_factory, count, width, channels, rate, keep, seed):
