@@ -78,6 +78,26 @@ def fuzz_clip(n, log_amp, seed, silence, integral):
     return x.astype(np.float32)
 
 
+def mel_conditioned(frames, fft_n, fb):
+    """Frames whose every mel energy stands clear of the FFT's rounding noise:
+    min_m e_m >= 1e-9 max_m e_m over the bank's non-empty filters (or the
+    frame is silent).  A band on an exact spectral null -- a frame of two
+    +-1 samples d apart zeroes every bin k with k d / fft_n integral -- has
+    energy 0 in exact arithmetic and float32 rounding noise in the oracle's
+    (the reference's) FFT: 1.4e-37 where the device's DFT gives 0 -> eps, so
+    that filter's log-energy, and the MFCC, are the noise's, not the
+    signal's.  Found by a deep fuzz run (VAD_FUZZ_SEED=9001: frame_len 115,
+    stride 92, fft_n 300, 40 filters, amplitude 10^-0.75 rounded to
+    integers); the tolerance of the other frames is unchanged."""
+    frames = list(frames)
+    if not frames:
+        return np.zeros(0, bool)
+    spec = O.spec_batch(np.stack(frames), fft_n).astype(np.float64)
+    e = spec @ fb[fb.sum(axis=1) > 0].T
+    emax = e.max(axis=1)
+    return (emax == 0) | (e.min(axis=1) >= 1e-9 * emax)
+
+
 def assert_mfcc_close(got, ref):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
@@ -111,7 +131,8 @@ def test_fuzz_clip_path(torch_cuda, nets, n, log_amp, seed, silence, i16, offlin
     assert m.shape == (F, 13)
     mc = m.cpu().numpy()
     fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
-    assert_mfcc_close(mc, O.mfcc_batch(clip, fb) if F else np.zeros((0, 13)))
+    ok = mel_conditioned(O.frame_matrix(clip), 512, fb)
+    assert_mfcc_close(mc[ok], (O.mfcc_batch(clip, fb) if F else np.zeros((0, 13)))[ok])
     lab = pipe.labels(a).cpu().numpy()
     assert lab.shape == (max(F - 5, 0),)
     if i16:
@@ -427,7 +448,8 @@ def test_fuzz_frame_matrix_mfcc(torch_cuda, frame_len, stride, n, nf, fft_n, log
     got = plan.mfcc(a, frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
     frames = np.stack([buf[i * stride:i * stride + frame_len] for i in range(n)])
     ref = np.stack([O.get_mfcc(f, fft_n, fb, 13) for f in frames])
-    assert_mfcc_close(got, ref)
+    ok = mel_conditioned(frames, fft_n, fb)
+    assert_mfcc_close(got[ok], ref[ok])
     got16 = plan.mfcc(a.to(torch.int16), frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
     np.testing.assert_array_equal(got16, got)
     spec = plan.spec(a, frame_len=frame_len, frame_stride=stride, n=n).cpu().numpy()
