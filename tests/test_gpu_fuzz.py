@@ -157,6 +157,44 @@ def test_fuzz_clip_path(torch_cuda, nets, n, log_amp, seed, silence, i16, offlin
     np.testing.assert_array_equal(lab[ok], O.ffn_labels(x, lay)[ok])
 
 
+@fuzz(12)
+@given(F=st.integers(2_000, 120_000), tail=st.integers(0, 159), log_amp=st.floats(-1.0, 4.6),
+       seed=st.integers(0, 2 ** 32 - 1), silence=st.one_of(st.none(), st.tuples(st.floats(0, 1), st.floats(0, 1))),
+       offline=st.booleans(), topo=st.sampled_from(["ref39", "bl13"]))
+def test_fuzz_large_clip_partitions(torch_cuda, nets, F, tail, log_amp, seed, silence, offline, topo):
+    """Clips of 2k..120k frames: the MFCC kernel's runs of 64-frame tiles and
+    the fused kernel's window ranges [n_win b / G, n_win (b + 1) / G) fall at
+    arbitrary places (test_fuzz_clip_path's clips give most workgroups one
+    tile or none, the full-size tests a few fixed sizes).  Every frame's MFCC
+    vs the oracle, fused labels == two-kernel labels, int16 == fp32, labels
+    vs the oracle's forward where its margin is decisive."""
+    import torch
+    from vad_amd import _lib
+    from vad_amd import plan as P
+    from vad_amd.ffn import FFNClassifier
+    from vad_amd.pipeline import VadPipeline
+    n = 160 * (F - 1) + 401 + tail
+    clip = fuzz_clip(n, log_amp, seed, silence, integral=True)
+    assert O.n_frames(n) == F
+    lay = nets[topo]
+    pipe = VadPipeline(FFNClassifier(lay), mode="offline" if offline else "analyser")
+    a = torch.from_numpy(clip).cuda()
+    m = pipe.mfcc(a)
+    mc = m.cpu().numpy()
+    fb = O.get_mel_filterbanks(300, 8000, 512, 26, 16000)
+    ok = mel_conditioned(O.frame_matrix(clip), 512, fb)
+    assert_mfcc_close(mc[ok], O.mfcc_batch(clip, fb)[ok])
+    lab = pipe.labels(a).cpu().numpy()
+    assert torch.equal(pipe.mfcc(a.to(torch.int16)), m)
+    if pipe.fusable:
+        np.testing.assert_array_equal(pipe.labels(a, fused=True).cpu().numpy(), lab)
+    mode = _lib.FEAT_OFFLINE if offline else _lib.FEAT_ANALYSER
+    x = P.window_features(m, mode).cpu().numpy().astype(np.float64)[:, :lay[0][0].shape[0]]
+    okl = O.ffn_margin(x, lay) > MARGIN_TOL
+    np.testing.assert_array_equal(lab[okl], O.ffn_labels(x, lay)[okl])
+    assert okl.mean() > 0.5
+
+
 @fuzz(50)
 @given(S=st.integers(1, 70), T=st.integers(6, 40), K=st.sampled_from([1, 2, 3, 8]),
        log_amp=st.floats(-1.0, 4.6), seed=st.integers(0, 2 ** 32 - 1), kernel=st.sampled_from(["hop", "three"]),
