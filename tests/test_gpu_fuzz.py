@@ -98,15 +98,20 @@ def mel_conditioned(frames, fft_n, fb):
     return (emax == 0) | (e.min(axis=1) >= 1e-9 * emax)
 
 
-def assert_mfcc_close(got, ref):
+def assert_mfcc_close(got, ref, floor=None):
+    """The MFCC tolerance (test_gpu_parity): per frame ||d|| <= 1e-4 ||ref||
+    and max |d| <= 1e-4 max |ref|.  floor (per frame) bounds both
+    denominators from below -- for banks where the kept coefficients can
+    cancel (test_fuzz_get_mfcc_any_bank)."""
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)
     assert got.shape == ref.shape
     if len(ref) == 0:
         return
     d = got - ref
-    rel = np.linalg.norm(d, axis=1) / np.linalg.norm(ref, axis=1)
-    mx = np.abs(d).max(axis=1) / np.abs(ref).max(axis=1)
+    fl = 0.0 if floor is None else np.asarray(floor, np.float64)
+    rel = np.linalg.norm(d, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), fl)
+    mx = np.abs(d).max(axis=1) / np.maximum(np.abs(ref).max(axis=1), fl)
     assert rel.max() <= MFCC_TOL, (rel.max(), int(rel.argmax()))
     assert mx.max() <= MFCC_TOL, (mx.max(), int(mx.argmax()))
 
@@ -361,9 +366,17 @@ def test_fuzz_get_mfcc_any_bank(torch_cuda, fft_n, n_filters, mfcc_frac, low, hi
     got = M.get_mfcc(frame, fft_n, fb, mfcc_n)
     ref = O.get_mfcc(frame, fft_n, fb, mfcc_n)
     assert got.shape == ref.shape == (mfcc_n,)
-    assert_mfcc_close(got[None], ref[None])
+    # the kept coefficients of the orthonormal DCT can cancel (2 filters, c0
+    # only: log-energies -0.2165 and +0.2155 give c0 = -7e-4, deep run seed
+    # 2323) while their rounding error scales with the log-mel row: the
+    # denominators are floored at its RMS (|| full DCT || / sqrt(n_filters))
     spec = O.get_spec_mag(frame, fft_n)
-    assert_mfcc_close(M.get_mfcc_from_spec(spec, fb, mfcc_n)[None], O.get_mfcc_from_spec(spec, fb, mfcc_n)[None])
+    e = spec.astype(np.float64) @ fb.T
+    lm = np.log10(np.where(e == 0, np.finfo(float).eps, e))
+    floor = np.linalg.norm(lm) / np.sqrt(n_filters)
+    assert_mfcc_close(got[None], ref[None], floor=floor)
+    assert_mfcc_close(M.get_mfcc_from_spec(spec, fb, mfcc_n)[None], O.get_mfcc_from_spec(spec, fb, mfcc_n)[None],
+                      floor=floor)
 
 
 class _MarginRecorder:
