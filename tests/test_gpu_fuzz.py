@@ -597,8 +597,13 @@ def test_fuzz_ffn_any_topology(torch_cuda, dims, arith, log_scale, nan_rows, see
     # non-vacuous: the bound (1e-4, ~6x a worst-case f32 / split-f16 rounding
     # of four 64-term layers) is loose for deep networks: 82-95 % of the rows
     # are checked in the deep runs' narrowest cases (dims [48, 21, 26, 2, 2],
-    # [40, 1, 54, 14, 3], [2, 3, 54, 2, 4]), ~99 % typically
-    assert ok.mean() > 0.5
+    # [40, 1, 54, 14, 3], [2, 3, 54, 2, 4]), ~99 % typically.  A network whose
+    # width-1 layers collapse every row onto a few logit vectors (dims
+    # [33, 1, 1, 1, 3], deep run seed 3131: one near-tied vector) may leave
+    # none to check
+    z, _ = O.ffn_forward(x, lay)
+    collapsed = len(np.unique(np.round(z[np.isfinite(z).all(axis=1)], 9), axis=0)) < 10
+    assert collapsed or ok.mean() > 0.5
 
 
 @fuzz(30)
