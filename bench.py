@@ -576,11 +576,20 @@ def main():
         dom_ms, dom_bytes, dom = (mfcc_ms, MFCC_BYTES_PER_FRAME, "mfcc_kernel") \
             if mfcc_ms >= ffn_ms else (ffn_ms, FFN_BYTES_PER_FRAME, "ffn_kernel")
         achieved = dom_bytes * F / (dom_ms * 1e-3) / 1e9
-        traffic = None
+        # roofline.traffic is NOT measured in this run (a PMC pass cannot run
+        # inside the timed process): it is read from the committed rocprofv3
+        # --pmc FETCH_SIZE / WRITE_SIZE pass (profiles/pmc_traffic.json), and
+        # traffic_source says which run produced it
+        traffic, traffic_source = None, None
         tp = os.path.join(REPO, "profiles", "pmc_traffic.json")
         if os.path.exists(tp):
             with open(tp) as f:
-                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            traffic = tj.get(dom, {}).get("hbm_bytes_per_launch")
+            if traffic is not None:
+                traffic_source = {"file": "profiles/pmc_traffic.json", "measured_in_this_run": False,
+                                  "run": tj.get("source"), "kernel": tj.get(dom, {}).get("kernel"),
+                                  "correction": tj.get("correction")}
         out = {
             "metric": "MFCC+FFN frames/sec on 16 kHz 25 ms/10 ms hop",
             "value": value,
@@ -615,6 +624,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_source,
                          "frac_vs_measured_copy": achieved / HBM_COPY_GBS,
                          "algorithmic_bytes_per_launch": dom_bytes * F,
                          "avg_launch_ms": dom_ms},

@@ -48,3 +48,35 @@ def label_agreement(got, ref, margin, name=None, extra=None):
         except OSError:
             pass
     return rep
+
+
+def record_vs_baseline(name, values):
+    """Write `values` beside the previous round's committed numbers
+    (profiles/regression_baseline.json) to gpurun_out/<name>.json, with an
+    `increased` flag per key: a kernel time past `flag_time_ratio` x its
+    baseline, a disagreement count above it.  A record, not a bound: the
+    tests' own gates stay as they are, the flags make drifts visible."""
+    root = os.environ.get("GRAFT_REPO_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {}
+    bp = os.path.join(root, "profiles", "regression_baseline.json")
+    if os.path.exists(bp):
+        with open(bp) as f:
+            base = json.load(f)
+    ratio = float(base.get("flag_time_ratio", 1.1))
+    rec = {"source": base.get("source"), "values": {}}
+    for k, v in values.items():
+        b = base.get(k)
+        inc = None
+        if b is not None:
+            inc = bool(v > b * ratio) if k.endswith("_ms") else bool(v > b)
+        rec["values"][k] = {"now": v, "baseline": b, "increased": inc}
+        if inc:
+            print(f"REGRESSION FLAG {name}: {k} = {v} vs baseline {b}", flush=True)
+    d = os.path.join(root, "gpurun_out")
+    try:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, name + ".json"), "w") as f:
+            json.dump(rec, f, indent=1)
+    except OSError:
+        pass
+    return rec

@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import vad_oracle as O
-from label_report import label_agreement
+from label_report import label_agreement, record_vs_baseline
 
 pytestmark = pytest.mark.gpu
 
@@ -143,6 +143,7 @@ def test_c3_full_clip_vs_oracle(torch_cuda):
     assert all(d["margin"] < FP32_MARGIN for d in rep["disagree_windows"]), rep["disagree_windows"]
     n_near = int((marg < FP32_MARGIN).sum())
     assert rep["disagree"] <= n_near, (rep["disagree"], n_near)
+    record_vs_baseline("c3_label_disagree", {"c3_label_disagree": rep["disagree"]})
     print(f"C3 labels: {rep['disagree']} of {F - 5} windows differ from the fp64 oracle, "
           f"{n_near} windows below the fp32 margin {FP32_MARGIN}")
     # and exactly the oracle's FFN on the device's own features where the
@@ -400,5 +401,8 @@ def test_kernel_time_guard(torch_cuda):
     t_mfcc = median_ms(lambda: pipe.mfcc(a, out=m))
     t_ffn = median_ms(lambda: plan.window_labels(m, out=lab))
     print(f"kernel time guard: MFCC {t_mfcc * 1e3:.1f} us, FFN {t_ffn * 1e3:.1f} us per 1M frames")
+    # recorded beside the previous round's driver times, increases flagged
+    # (gpurun_out/kernel_time_guard.json)
+    record_vs_baseline("kernel_time_guard", {"mfcc_kernel_ms": t_mfcc, "ffn_kernel_ms": t_ffn})
     assert t_mfcc < 2 * 0.245, t_mfcc
     assert t_ffn < 2 * 0.052, t_ffn

@@ -297,6 +297,9 @@ def test_ffn_label_difference_overflowed_logits(torch_cuda):
         clf = FFNClassifier(lay_s)
         lab = clf.plan.window_labels(m).cpu().numpy()
         lab_l, zl = (t.cpu().numpy() for t in P.window_logits(clf.plan, m))
+        # the logits launch takes its labels from the same difference: a
+        # label never depends on whether the logits were requested
+        np.testing.assert_array_equal(lab, lab_l)
         np.testing.assert_array_equal(lab[flag], 0)
         # fp64 hidden activations of the scaled network, and the device's f32
         # difference weights (class 1 minus class 0 of the f32 plan weights)

@@ -233,3 +233,45 @@ def test_hop_rows_disjoint_layouts():
     assert not hop_rows_disjoint(S, K, 3 * H, H, H)        # blocks overlap
     assert not hop_rows_disjoint(S, K, H, K * H - 1, H)    # stream rows overlap
     assert not hop_rows_disjoint(S, K, H - 1, K * H, H)    # a stream's hops overlap each other
+
+
+def _device_disassembly(tmp_path):
+    """Disassembly of every gfx950 code object bundled in the built library."""
+    import shutil
+    import subprocess
+    from vad_amd import _lib
+    llvm = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(llvm):
+        pytest.skip("llvm-objdump not in this image")
+    so = tmp_path / "lib.so"
+    shutil.copy(_lib.LIB_PATH, so)
+    subprocess.run([llvm, "--offloading", str(so)], cwd=tmp_path, check=True, capture_output=True)
+    out = []
+    for f in sorted(tmp_path.iterdir()):
+        if "gfx950" in f.name:
+            out.append(subprocess.run([llvm, "-d", str(f)], capture_output=True, text=True, check=True).stdout)
+    assert out, "no gfx950 code object in the library"
+    return "\n".join(out)
+
+
+def test_hop_kernel_waits_for_lds_dma_before_barrier(tmp_path):
+    """The hop kernel stages its tables with LDS-DMA (global_load_lds), whose
+    writes count on vmcnt; every workgroup barrier after the DMA must be
+    preceded by a vmcnt(0) wait in the same basic block, or a wave could read
+    a table another wave's DMA has not landed yet (stream_kernel.hip)."""
+    dis = _device_disassembly(tmp_path)
+    funcs = re.split(r"\n(?=[0-9a-f]+ <)", dis)
+    hop = [f for f in funcs if re.match(r"[0-9a-f]+ <_ZN3vad17stream_hop_kernel", f)]
+    assert hop, "stream_hop_kernel not found"
+    for f in hop:
+        lines = f.splitlines()
+        assert any("global_load_lds" in l for l in lines)
+        dma = next(i for i, l in enumerate(lines) if "global_load_lds" in l)
+        bars = [i for i, l in enumerate(lines) if re.search(r"\bs_barrier\b", l) and i > dma]
+        assert bars
+        for b in bars:
+            k = b - 1
+            while k > dma and not re.search(r"s_waitcnt\s+vmcnt\(0\)", lines[k]):
+                assert not re.search(r"\bs_(cbranch|branch)", lines[k]), "barrier not dominated by a vmcnt(0) wait"
+                k -= 1
+            assert k > dma, lines[b]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of library variants (vad_amd/lib/libvad_amd_<name>.so): tools/r03_ab.sh <tag> <rounds> <name>...
+# A/B of library variants (vad_amd/lib/libvad_amd_<name>.so): tools/ab_mfcc_variants.sh <tag> <rounds> <name>...
 set -u
 TAG=$1; N=$2; shift 2
 R=$GRAFT_REPO_ROOT

@@ -10,4 +10,4 @@ mkdir -p gpurun_out/$TAG
 VAD_MFCC_BALANCE_DEBUG=100 timeout -k 10 200 python3 tools/mel40_probe.py > gpurun_out/$TAG/probe.json 2> gpurun_out/$TAG/speeds.txt || exit 1
 grep balance gpurun_out/$TAG/speeds.txt | head -3
 cp vad_amd/lib/libvad_amd.so vad_amd/lib/libvad_amd_bal.so
-bash tools/r03_ab.sh $TAG 3 nobal bal
+bash tools/ab_mfcc_variants.sh $TAG 3 nobal bal

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round 4 validation after the matrix-core kernel was withdrawn: GPU tests,
+# Full validation: GPU tests,
 # smoke, default bench, the bench's own 2-rank launcher (gloo, one GPU), then
 # the kernel trace + PMC passes (tools/profile.sh).  Stops at the first failure.
 set -u
-TAG=${1:-r04c}
+TAG=$1
 R=$GRAFT_REPO_ROOT
 cd $R
 bash tools/validate.sh $TAG || exit $?

@@ -720,18 +720,26 @@ __device__ __forceinline__ int wave_tile_classify(const float* __restrict__ X, c
   return wave_tile_mlp<KS0, T1, T2, T3, T4, NC, NOVL, IN_BOUNDED>(x0, wnan, fh, fb, fv, n_classes, z);
 }
 
-// Label of window lane & 15 by the logit difference (valu_label2): the
-// labels-only launches of a 13-64-64-2-shaped network; fd = the lane group's
-// difference slots (TI*4 weights, then the bias).
+// Label of window lane & 15 by the logit difference (valu_label2): every
+// launch of a 13-64-64-2-shaped network; fd = the lane group's difference
+// slots (TI*4 weights, then the bias).  z (when given: launches that also
+// write the logits) receives the two logits from the same hidden layer, so a
+// window's label never depends on whether its logits were requested.
 template <int KS0, int T1, int T2, int IN, int XS, bool MASK, bool IN_BOUNDED, class FH, class FB, class FV, class FD>
 __device__ __forceinline__ int wave_tile_label2(const float* __restrict__ X, const int* __restrict__ FL, int lane,
-                                                FH fh, FB fb, FV fv, FD fd, int h1_bounded) {
+                                                FH fh, FB fb, FV fv, FD fd, int h1_bounded,
+                                                f32x4* z = nullptr) {
   constexpr int K0 = (4 * KS0 + 31) / 32;
   using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
   float x0[K0][8];
   const int wnan = wave_tile_operands<K0, IN, XS, MASK>(X, FL, lane, x0);
   f32x4 h2[T2];
   mlp_hidden2_h3<KS0, T1, T2, FB, IN_BOUNDED>(fh, fb, x0, h2, h1_bounded != 0);
+  if (z) {
+    f32x4 zz = valu_out_layer<TP, T2, FV>(fv, h2);
+    if (wnan) zz = (f32x4){__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    *z = zz;
+  }
   return valu_label2<TP, T2>(fd, fv, h2, wnan);
 }
 

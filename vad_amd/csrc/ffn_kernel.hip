@@ -416,8 +416,11 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   constexpr bool kLdsFrags = WaveResidency<KS0, NC>::kLdsFrags;
   constexpr bool kLdsSlots = WaveResidency<KS0, NC>::kLdsSlots;
   constexpr int NSL = TP::NB + TP::NV + TP::NVB;  // bias + output-layer slots
-  // the logit-difference slots (valu_label2): TIL*4 weights, then the bias
-  constexpr bool kDiff = !LG && NC == 2 && TP::VL && TP::NL == 3 && kLdsSlots;
+  // the logit-difference slots (valu_label2): TIL*4 weights, then the bias.
+  // Launches that also write the logits (LG) take their labels from the same
+  // difference (a label must not depend on whether the logits
+  // were requested)
+  constexpr bool kDiff = NC == 2 && TP::VL && TP::NL == 3 && kLdsSlots;
   constexpr int NSD = kDiff ? TP::TIL * 4 + 1 : 0;
   constexpr int NSLP = (NSL + NSD + 3) & ~3;
   __shared__ __attribute__((aligned(16))) float slot_s[kLdsSlots ? 4 * NSLP : 1];
@@ -541,7 +544,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     int lab;
     if constexpr (kDiff) {
       lab = wave_tile_label2<KS0, T1, T2, IN, XS, false, wave_tile_in_bounded<MODE, IN>>(
-          X, FL, lane, fh, fbs, fvs, LdsRow{slot_s + g * NSLP + NSL}, net.h1_bounded);
+          X, FL, lane, fh, fbs, fvs, LdsRow{slot_s + g * NSLP + NSL}, net.h1_bounded, LG ? &z : nullptr);
     } else {
       lab = wave_tile_classify<KS0, T1, T2, T3, T4, NC, VAD_FFN_WAVE_MFMA_OUT != 0, IN, XS, false,
                                wave_tile_in_bounded<MODE, IN>>(X, FL, lane, fh, fbs, fvs, net.n_classes, z);
@@ -554,7 +557,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
     const int64_t w = t * kWTile + jw;
     if (g == 0 && w < n_rows) {
       labels[w] = (uint8_t)lab;
-      if constexpr (!kDiff) store_logits(net.logits, w, z, net.n_classes);
+      if constexpr (LG) store_logits(net.logits, w, z, net.n_classes);
     }
   };
   // kPF tiles per trip (VAD_FFN_PF; 1 in the all-LDS residency, whose

@@ -74,11 +74,20 @@ __global__ __launch_bounds__(kSimpleThreads) void simple_features_kernel(
     for (int k = t; k < L; k += kSimpleThreads) {
       double ar = 0.0, ai = 0.0;
       int kn = 0;
+      // twiddle exp(-2 pi i kn / L): exact (sincospi) every 16th term, a
+      // rotation by exp(-2 pi i k / L) in between -- 16x fewer sincospi than
+      // one per term (an 8193-point frame made 67M calls), each twiddle
+      // within ~16 roundings of the exact one
+      double sk, ck;
+      sincospi(-2.0 * (double)k / (double)L, &sk, &ck);
+      double s = 0.0, c = 1.0;
       for (int n = 0; n < L; ++n) {
-        double s, c;
-        sincospi(-2.0 * (double)kn / (double)L, &s, &c);
+        if ((n & 15) == 0) sincospi(-2.0 * (double)kn / (double)L, &s, &c);
         ar += re[n] * c;
         ai += re[n] * s;
+        const double c2 = c * ck - s * sk;
+        s = fma(s, ck, c * sk);
+        c = c2;
         kn += k;
         if (kn >= L) kn -= L;
       }
@@ -227,15 +236,24 @@ hipError_t launch_simple_features(const float* frames, int64_t n_frames, int fra
   if (L > kSimpleMaxL) return hipErrorInvalidValue;
   if ((L & (L - 1)) == 0) {
     // waves per block: as many (up to 4) as the LDS holds beside the twiddle
-    // table (L = 512: 36 KB; 2048: 144 KB; 4096: one wave, 96 KB; 8192: one
-    // wave, 128 KB, twiddles computed per butterfly)
+    // table (L = 512: 36 KB; 2048: 144 KB; 4096: 32 KB of twiddles + two
+    // waves x 64 KB = 160 KB, the whole budget -- the kernel declares no
+    // static LDS, checked below; 8192: one wave, 128 KB, twiddles computed
+    // per butterfly)
     const int tw_lds = L <= 4096;
     const size_t tw_bytes = tw_lds ? (size_t)L * sizeof(double) : 0;
     const size_t wave_bytes = (size_t)2 * L * sizeof(double);
     int waves = 4;
     while (waves > 1 && tw_bytes + waves * wave_bytes > (size_t)kSimpleLds) --waves;
     const size_t smem = tw_bytes + waves * wave_bytes;
-    if (smem > (size_t)kSimpleLds) return hipErrorInvalidValue;
+    static size_t static_lds = ~(size_t)0;  // the kernel's own __shared__ bytes (0 today)
+    if (static_lds == ~(size_t)0) {
+      hipFuncAttributes fa{};
+      if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&simple_features_wave_kernel)) != hipSuccess)
+        return hipErrorInvalidValue;
+      static_lds = fa.sharedSizeBytes;
+    }
+    if (smem + static_lds > (size_t)kSimpleLds) return hipErrorInvalidValue;
     static std::atomic<unsigned long long> attr_done{0};
     hipError_t e = ensure_dyn_lds(reinterpret_cast<const void*>(&simple_features_wave_kernel), kSimpleLds, attr_done);
     if (e != hipSuccess) return e;

@@ -260,7 +260,13 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
 #pragma unroll
     for (int q = 0; q < 4; ++q) tws[q] = tw_g[lane + 64 * q];
   }
-  __syncthreads();  // the staged tables are complete (the barrier waits for the LDS-DMA)
+  // the staged tables are complete: LDS-DMA writes count on vmcnt, not
+  // lgkmcnt, and a workgroup-scope release fence need not drain vmcnt, so the
+  // wait is explicit (vmcnt 0, before the barrier; the state and twiddle
+  // loads above are needed right after it anyway).  Locked by
+  // test_hop_kernel_waits_for_lds_dma_before_barrier (the built ISA).
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0, expcnt 7, lgkmcnt 15
+  __syncthreads();
   if (s >= n_streams) return;  // wave-uniform; no barrier below
   float* scr = hsm + wv * kHopWaveFloats;
   float2* z0 = reinterpret_cast<float2*>(scr);
