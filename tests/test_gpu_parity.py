@@ -91,6 +91,37 @@ def test_mfcc_from_spec_vs_reference(torch_cuda, golden, fb26):
     assert_mfcc_close(MfccPlan(fb26).from_spec(s).cpu().numpy(), g["mfcc26"])
 
 
+def test_spectral_null_frames(torch_cuda, golden):
+    """Frames with exact spectral nulls (tests/golden/nulls.npz, made by the
+    unmodified reference: cyclotomic impulse combs).  At
+    the reference configuration only filter 9 of the 40-filter bank can lie
+    wholly on null bins (tests/test_oracle_golden.py proves it from the
+    banks), and three fixture frames null it: there the reference's energy
+    is exactly 0 -> eps.  The device's spectrum is exactly 0 on every exact
+    null bin (frame path, and the clip path for a one-frame clip), so its
+    null filter gives the same deterministic log10(eps), and its MFCCs match
+    the reference's within the MFCC rule on every frame, 26 and 40 filters."""
+    torch = torch_cuda
+    from vad_amd.pipeline import VadPipeline
+    from vad_amd.config import MfccConfig
+    from vad_amd.plan import MfccPlan
+    g = golden("nulls")
+    fr, nb = g["frames"], g["null_bins"]
+    t = torch.from_numpy(fr).cuda()
+    spec = MfccPlan(O.get_mel_filterbanks(300, 8000, 512, 26, 16000)).spec(t).cpu().numpy()
+    np.testing.assert_array_equal(spec[nb], 0.0)
+    assert frame_rel(spec, g["spec"]).max() <= SPEC_TOL
+    fb40 = O.get_mel_filterbanks(300, 8000, 512, 40, 16000)
+    null9 = nb[:, np.flatnonzero(fb40[9])].all(axis=1)
+    assert null9.sum() >= 3 and ((g["spec"] @ fb40.T)[null9, 9] == 0).all()
+    for nf in (26, 40):
+        fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+        assert_mfcc_close(MfccPlan(fb).mfcc(t).cpu().numpy(), g[f"mfcc{nf}"])
+        pipe = VadPipeline(cfg=MfccConfig(n_filters=nf))
+        clip = np.stack([pipe.mfcc(t[i].contiguous()).cpu().numpy()[0] for i in range(len(fr))])
+        assert_mfcc_close(clip, g[f"mfcc{nf}"])
+
+
 @pytest.mark.parametrize("L", [800, 512, 256, 401])
 def test_other_frame_lengths(torch_cuda, golden, fb26, L):
     """np.fft.fft(x, 512) truncates frames > 512 and zero-pads short ones."""

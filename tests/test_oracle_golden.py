@@ -235,3 +235,54 @@ def test_ffn_oracle_matches_sklearn_mlp(golden, topo, n_classes):
     sp = clf.predict_proba(x)
     np.testing.assert_allclose(sp, p, rtol=0, atol=1e-12)
     np.testing.assert_array_equal(clf.predict(x), O.ffn_labels(x, layers))
+
+
+def _cyclotomic_degree(taps, fft_n):
+    """Least degree of a nonzero rational polynomial vanishing at w^k for
+    every k in taps (w = exp(-2 pi i / fft_n), fft_n a power of two): the sum
+    of phi(m) over the distinct orders m = fft_n / gcd(k, fft_n) -- X[k] = 0
+    for a frame with rational samples x iff Phi_m divides sum x[n] z^n, and
+    distinct cyclotomic polynomials are coprime."""
+    from math import gcd
+    orders = {fft_n // gcd(int(k), fft_n) for k in taps}
+    return sum(1 if m == 1 else m // 2 for m in orders)
+
+
+def test_spectral_null_reachability():
+    """Which mel filters can lie wholly on exact spectral nulls (energy
+    exactly 0 -> eps in exact arithmetic, rounding noise in an FFT that does
+    not cancel exactly) for a reference-configuration frame: 400 samples
+    zero-padded to 512, so sum x[n] z^n has degree <= 399.  26 filters: none
+    (the least degree is 400, filter 1, bins 13..17).  40 filters: filter 9
+    alone (bins 30..33: Phi_256 Phi_512 Phi_16, degree 392), and the
+    fixture's (z^256+1)(z^128+1)(z^8+1) frames null it exactly -- checked in
+    exact cyclotomic arithmetic (gen_nulls.exact_null_bins), not by FFT."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from gen_nulls import comb_frames, exact_null_bins
+    deg = {}
+    for nf in (26, 40):
+        fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+        deg[nf] = [_cyclotomic_degree(np.flatnonzero(fb[m]), 512) for m in range(nf)]
+    assert min(deg[26]) == 400 and deg[26].index(400) == 1
+    assert [m for m in range(40) if deg[40][m] <= 399] == [9] and deg[40][9] == 392
+    fb40 = O.get_mel_filterbanks(300, 8000, 512, 40, 16000)
+    taps9 = np.flatnonzero(fb40[9])
+    hit = [i for i, f in enumerate(comb_frames()) if exact_null_bins(f)[taps9].all()]
+    assert len(hit) >= 3
+    # the deep-fuzz configuration (fft_n 300 is not a power of two: Phi_m of
+    # other orders; the reachability there is what test_gpu_fuzz excludes)
+
+
+def test_null_fixture_pins_oracle(golden):
+    """The oracle on the spectral-null fixture (tests/golden/nulls.npz, the
+    reference's own outputs): spectra bit-exact (pocketfft), exact zeros on
+    every exact null bin, MFCCs within 1e-6 at 26 and 40 filters."""
+    g = golden("nulls")
+    spec = O.spec_batch(g["frames"], 512)
+    np.testing.assert_array_equal(spec, g["spec"])
+    np.testing.assert_array_equal(spec[g["null_bins"]], 0.0)
+    for nf in (26, 40):
+        fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
+        m = np.stack([O.get_mfcc_from_spec(s, fb, 13) for s in spec])
+        np.testing.assert_allclose(m, g[f"mfcc{nf}"], rtol=1e-6, atol=1e-6)

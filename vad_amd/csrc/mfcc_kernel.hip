@@ -650,24 +650,40 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
       }
     }
     const int64_t flast = n_frames - 1;
-    // frame-granular, balanced runs: workgroup b owns frames
-    // [b F / G, (b + 1) F / G) in 64-frame tiles of its own; in a last,
-    // partial tile the waves whose frames all lie past the run skip phase 1
-    // (a tile-granular split leaves F / 64 mod G workgroups one full extra
-    // tile: a 7-tile makespan for 6.1 tiles of work at 100k frames)
-    // (frame-granular runs measured C2 -1.6 %, C3 +0.7 %: tile runs kept)
+    // Runs of 32-frame units: workgroup b owns frames [32 u_b, 32 u_(b+1)),
+    // u_b = b U / G over the clip's U = ceil(F / 32) units, in 64-frame
+    // tiles from its start; a run of an odd number of units ends in a HALF
+    // tile of <= 32 frames, which every wave runs as pass 0 only (lane group
+    // grp: frame f0 + grp), so its phase 1 costs about half a tile on all
+    // eight waves instead of a full tile's (C2, 100k frames: 12.2 units of
+    // work per workgroup, a makespan of 6.5 tiles instead of 7; C3: 61.5
+    // instead of 62).  (Frame-granular runs with one wave running the last
+    // few frames measured C2 -1.6 %, C3 +0.7 % in round 5: a lone wave on its
+    // SIMD issues at a third of a pair's rate.)  XCD-balanced runs
+    // (MfccBalance word != 0) stay tile-granular.
     // tile runs balanced over the XCDs' clocks (MfccBalance; word 0: equal)
     const unsigned long long rt0 = bal.stats ? __builtin_amdgcn_s_memrealtime() : 0;
-    const int64_t f_beg = balanced_tile(bal.word, n_tiles, blockIdx.x, gridDim.x) * kTile;
-    const int64_t f_end0 = balanced_tile(bal.word, n_tiles, blockIdx.x + 1, gridDim.x) * kTile;
+    int64_t f_beg, f_end0;
+    if (bal.word == 0) {
+      const int64_t n_units = (n_frames + 31) / 32;
+      f_beg = (int64_t)blockIdx.x * n_units / gridDim.x * 32;
+      f_end0 = ((int64_t)blockIdx.x + 1) * n_units / gridDim.x * 32;
+    } else {
+      f_beg = balanced_tile(bal.word, n_tiles, blockIdx.x, gridDim.x) * kTile;
+      f_end0 = balanced_tile(bal.word, n_tiles, blockIdx.x + 1, gridDim.x) * kTile;
+    }
     const int64_t f_end = f_end0 < n_frames ? f_end0 : n_frames;
+    int64_t tile = 0;  // local tile index
+    const int64_t t_end = (f_end - f_beg + kTile - 1) / kTile;
+    // the last tile is a half tile when it holds <= 32 frames
+    const int64_t t_half = (t_end > 0 && f_end - f_beg - (t_end - 1) * kTile <= kTile / 2) ? t_end - 1 : -1;
+    // lane group grp's first frame in tile t: 2 grp (paired passes) or grp
+    // (the half tile's single pass)
     auto pair_base = [&](int64_t t, int& lim) {
-      const int64_t F = f_beg + t * kTile + 2 * grp;
+      const int64_t F = f_beg + t * kTile + (t == t_half ? grp : 2 * grp);
       lim = F < flast ? 32 * HOPC + LEN - 2 : LEN - 2;
       return src + (F < flast ? F : flast) * frame_stride;
     };
-    int64_t tile = 0;  // local tile index
-    const int64_t t_end = (f_end - f_beg + kTile - 1) / kTile;
     v2f buf[NB];
     {
       int lim;
@@ -677,22 +693,31 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
     __builtin_amdgcn_sched_barrier(0);
     int64_t prev_f0 = -1;
     // one tile; its buffer is refilled with the next tile's chunks as it frees up
-    auto tile_body = [&](v2f (&buf)[NB]) {
+    auto tile_body = [&](auto half_tag, v2f (&buf)[NB]) {
+      constexpr bool HALF = decltype(half_tag)::value;
       const int64_t f0 = f_beg + tile * kTile;
-      const int64_t fa = f0 + 2 * grp, fb = fa + 1;
-      const bool active = f0 + 8 * wave < f_end;  // wave-uniform: some frame of the wave is in the run
+      const int64_t fa = f0 + (HALF ? grp : 2 * grp), fb = fa + 1;
+      // wave-uniform: some frame of the wave is in the run
+      const bool active = f0 + (HALF ? 4 : 8) * wave < f_end;
       float* prow_a;
       float* prow_b;
       if constexpr (MODE == kAudioToSpec) {
         prow_a = out + (fa < f_end ? fa : flast) * kBins;
         prow_b = out + (fb < f_end ? fb : flast) * kBins;
       } else {
-        prow_a = P + (2 * grp) * kPStride;
+        prow_a = P + (HALF ? grp : 2 * grp) * kPStride;
         prow_b = P + (2 * grp + 1) * kPStride;
       }
       int lim;
       const TIN* nb = pair_base(tile + 1, lim);
-      if (active) {  // phase 1
+      if (active && HALF) {  // phase 1, pass 0 only (the run's last tile: no prefetch)
+        v2f u[16], col[32];
+        stage_a_at<TIN, NZ, LEN, 0, NB, WIN>(buf, L, j, u, wv);
+        __builtin_amdgcn_sched_barrier(0);
+        store_a(u, gscr, j);
+        read_b(L, gscr, col);
+        if (MODE != kAudioToSpec || fa < f_end) finish_b<MODE == kAudioToSpec>(L, col, prow_a);
+      } else if (active) {  // phase 1
         v2f u[16], col[32];
         VAD_MILESTONE(3);
         stage_a_at<TIN, NZ, LEN, 0, NB, WIN>(buf, L, j, u, wv);
@@ -723,12 +748,18 @@ __global__ __launch_bounds__(kThreads, 1) void mfcc_kernel(
         if (prev_f0 >= 0 && wave < kDctGroups)
           phase2b_any<SPEC, true>(plan, lm, dtb, wave, lane, prev_f0, f_end, mfcc_n, out);
         lds_barrier();  // P complete; log-mel rows consumed
+        // (a half tile's rows 32..63 hold the previous tile's power: their
+        // log-mel rows are computed and never stored, phase 2b stops at f_end)
         phase2a<SPEC>(plan, P, lm, wave, lane);
         lds_barrier();  // log-mel rows complete; P and the FFT scratch free
         prev_f0 = f0;
       }
     };
-    for (; tile < t_end; ++tile) tile_body(buf);
+    for (; tile < (t_half >= 0 ? t_half : t_end); ++tile) tile_body(std::false_type{}, buf);
+    if (t_half >= 0) {
+      tile_body(std::true_type{}, buf);
+      ++tile;
+    }
 
     if constexpr (MODE == kAudioToMfcc) {
       if (prev_f0 >= 0 && wave < kDctGroups)
