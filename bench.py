@@ -282,7 +282,7 @@ def secondary_configs(dev, reps=60):
     # copy): each step copies the 512 x 160 new samples of its K hops from
     # pinned host memory, runs the hop kernel and copies the K x 512 labels
     # back (StreamBatch.step_host), launched directly or as ONE graph replay
-    # (vad_graph_launch) -- us_per_hop back to back, and latency_us = one
+    # (vad_graph_plan_launch) -- us_per_hop back to back, and latency_us = one
     # step until its labels are in host memory (stream sync, host clock).
     clf = FFNClassifier(random_layers(TOPOLOGY_BL13, seed=3))
     for name, kernel, K, graph, copy, host in (

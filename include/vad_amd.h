@@ -327,6 +327,18 @@ int vad_stream_step(const vad_mfcc_plan* plan, const vad_ffn_plan* ffn, const fl
  * is the host's (hipStreamBeginCapture / torch.cuda.graph); this entry only
  * launches, so a host replays without a runtime wrapper in between. */
 int vad_graph_launch(void* graph_exec, void* stream);
+/* The same replay, prepared once from the captured hipGraph_t and its
+ * hipGraphExec_t (StreamBatch.capture keeps both; the graph must outlive the
+ * plan): a graph of exactly one kernel node -- the one-hop step -- is
+ * dispatched as that node (its captured function, grid, block, dynamic LDS
+ * and argument values), whose host cost is a kernel launch's rather than
+ * hipGraphLaunch's (~5 us more per call on ROCm 7.2); any other graph goes
+ * through hipGraphLaunch.  vad_graph_plan_direct says which (1: the node). */
+typedef struct vad_graph_plan vad_graph_plan;
+int vad_graph_plan_create(void* graph, void* graph_exec, vad_graph_plan** out);
+int vad_graph_plan_launch(const vad_graph_plan* plan, void* stream);
+int32_t vad_graph_plan_direct(const vad_graph_plan* plan);
+int vad_graph_plan_destroy(vad_graph_plan* plan);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU clip sharding: one process per GPU, each

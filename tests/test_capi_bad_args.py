@@ -55,6 +55,8 @@ call("vad_stream_hop", N, N, N, 400, 400, N, 160, 160, 10, N, N, N, N)
 call("vad_stream_hops", N, N, N, 400, 400, N, 160, 160, 10, 8, 1600, N, N, N, 10, N)
 call("vad_stream_step", N, N, N, 400, 400, 10, N, N, N, N, N)
 call("vad_graph_launch", N, N)
+call("vad_graph_plan_create", N, N, N)
+call("vad_graph_plan_launch", N, N)
 call("vad_rccl_init", N, 1, N, 0)
 call("vad_rccl_gather_u8", N, N, N, 10, 0, N)
 # neutral values

@@ -194,6 +194,9 @@ def test_c5_512_streams_graph_replay(torch_cuda, golden, kernel):
     sb = StreamBatch(S, FFNClassifier(layers), kernel=kernel)
     sb.prime(torch.from_numpy(np.ascontiguousarray(clips[:, :240])).cuda())
     sb.capture()
+    # the one-hop capture is one kernel node, replayed as that node; the
+    # three-kernel step goes through hipGraphLaunch
+    assert sb.graph_direct == (kernel == "hop")
     hops = torch.from_numpy(np.ascontiguousarray(
         np.stack([clips[:, 240 + 160 * t: 400 + 160 * t] for t in range(T)]))).cuda()
     got = np.stack([sb.step(hops[t]).cpu().numpy().copy() for t in range(T)], axis=1)  # (S, T)

@@ -75,6 +75,10 @@ SIGNATURES = {
     "vad_stream_step": (c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp, c_vp,
                                 c_vp]),
     "vad_graph_launch": (c_int, [c_vp, c_vp]),
+    "vad_graph_plan_create": (c_int, [c_vp, c_vp, c_vp]),
+    "vad_graph_plan_launch": (c_int, [c_vp, c_vp]),
+    "vad_graph_plan_direct": (c_i32, [c_vp]),
+    "vad_graph_plan_destroy": (c_int, [c_vp]),
     "vad_rccl_available": (c_int, []),
     "vad_rccl_error_string": (ctypes.c_char_p, []),
     "vad_rccl_unique_id": (c_int, [c_vp]),

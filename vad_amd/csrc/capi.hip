@@ -905,4 +905,60 @@ int vad_graph_launch(void* graph_exec, void* stream) {
   return (int)hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream);
 }
 
+// A captured step prepared for replay.  A graph of exactly one kernel node
+// (the one-hop step of StreamBatch, kernel="hop") is dispatched as that
+// node: its captured function, grid, block, dynamic LDS and argument values
+// (kernelParams point into the graph's own copy, so the graph must outlive
+// the plan) go to hipLaunchKernel -- on ROCm 7.2 a hipGraphLaunch of one
+// kernel node costs ~5 us more host time per call than the launch it wraps
+// (profiles/r06/c5_graph/), so back-to-back one-hop replays were host-bound
+// at ~15 us against ~10 us launched directly.  Any other graph replays
+// through hipGraphLaunch.
+struct vad_graph_plan {
+  hipGraphExec_t exec;
+  int32_t n_nodes;
+  bool direct;
+  hipKernelNodeParams kp;
+};
+
+int vad_graph_plan_create(void* graph, void* graph_exec, vad_graph_plan** out) {
+  if (!graph || !graph_exec || !out) return VAD_EINVAL;
+  *out = nullptr;
+  size_t n = 0;
+  hipError_t e = hipGraphGetNodes((hipGraph_t)graph, nullptr, &n);
+  if (e != hipSuccess) return (int)e;
+  vad_graph_plan* p = (vad_graph_plan*)calloc(1, sizeof(vad_graph_plan));
+  if (!p) return VAD_ENOMEM;
+  p->exec = (hipGraphExec_t)graph_exec;
+  p->n_nodes = (int32_t)n;
+  p->direct = false;
+  if (n == 1) {
+    hipGraphNode_t node;
+    size_t one = 1;
+    hipGraphNodeType ty;
+    if (hipGraphGetNodes((hipGraph_t)graph, &node, &one) == hipSuccess && one == 1 &&
+        hipGraphNodeGetType(node, &ty) == hipSuccess && ty == hipGraphNodeTypeKernel &&
+        hipGraphKernelNodeGetParams(node, &p->kp) == hipSuccess && p->kp.func && p->kp.kernelParams &&
+        !p->kp.extra)
+      p->direct = true;
+  }
+  *out = p;
+  return VAD_OK;
+}
+
+int vad_graph_plan_launch(const vad_graph_plan* p, void* stream) {
+  if (!p) return VAD_EINVAL;
+  if (p->direct)
+    return (int)hipLaunchKernel(p->kp.func, p->kp.gridDim, p->kp.blockDim, p->kp.kernelParams,
+                                p->kp.sharedMemBytes, (hipStream_t)stream);
+  return (int)hipGraphLaunch(p->exec, (hipStream_t)stream);
+}
+
+int32_t vad_graph_plan_direct(const vad_graph_plan* p) { return p && p->direct ? 1 : 0; }
+
+int vad_graph_plan_destroy(vad_graph_plan* p) {
+  free(p);
+  return VAD_OK;
+}
+
 }  // extern "C"

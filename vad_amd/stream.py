@@ -35,6 +35,7 @@ reads ``inputs`` in place, so a producer that writes the next block there
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -209,8 +210,7 @@ class StreamBatch:
         self.host_labels.copy_(self.label_block, non_blocking=True)
 
     def _replay(self):
-        _lib.check(_lib.lib().vad_graph_launch(ctypes.c_void_p(self.graph.raw_cuda_graph_exec()),
-                                               _lib.stream_ptr()), "vad_graph_launch")
+        _lib.check(self._graph_launch(self._graph_plan, _lib.stream_ptr()), "vad_graph_plan_launch")
 
     def step_host(self):
         """One step (K hops) from ``host_inputs`` to ``host_labels``: H2D
@@ -247,9 +247,34 @@ class StreamBatch:
         torch.cuda.synchronize()
         self.frames.copy_(saved[0]); self.ring.copy_(saved[1])
         self.count.copy_(saved[2]); self.label_block.copy_(saved[3])
-        g = torch.cuda.CUDAGraph()
+        # keep_graph: the captured hipGraph_t stays alive beside its exec, so
+        # the replay plan can read its nodes (vad_graph_plan_create: a
+        # one-kernel-node graph -- the one-hop step -- is dispatched as its
+        # node, whose host cost is a launch's, not hipGraphLaunch's)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g):
             body()
+        g.instantiate()
+        self._drop_graph_plan()
+        lib = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(lib.vad_graph_plan_create(ctypes.c_void_p(g.raw_cuda_graph()),
+                                             ctypes.c_void_p(g.raw_cuda_graph_exec()), ctypes.byref(h)),
+                   "vad_graph_plan_create")
+        self._graph_plan = h
+        self._graph_launch = lib.vad_graph_plan_launch
+        self._graph_plan_free = weakref.finalize(self, lib.vad_graph_plan_destroy, h)
         self.graph = g
         self.graph_host_io = bool(host_io)
         return g
+
+    @property
+    def graph_direct(self):
+        """True when replays dispatch the captured graph's single kernel node."""
+        return self.graph is not None and bool(_lib.lib().vad_graph_plan_direct(self._graph_plan))
+
+    def _drop_graph_plan(self):
+        fin = getattr(self, "_graph_plan_free", None)
+        if fin is not None:
+            fin()  # the plan before the graph it points into
+        self._graph_plan = None
