@@ -118,7 +118,10 @@ def test_spectral_null_frames(torch_cuda, golden):
         fb = O.get_mel_filterbanks(300, 8000, 512, nf, 16000)
         assert_mfcc_close(MfccPlan(fb).mfcc(t).cpu().numpy(), g[f"mfcc{nf}"])
         pipe = VadPipeline(cfg=MfccConfig(n_filters=nf))
-        clip = np.stack([pipe.mfcc(t[i].contiguous()).cpu().numpy()[0] for i in range(len(fr))])
+        # one-frame clips: 401 samples (the reference's strict '>' framing,
+        # file_processing.py:80-103, takes no frame from exactly 400)
+        one = torch.cat([t, torch.zeros((len(fr), 1), device=t.device)], dim=1)
+        clip = np.stack([pipe.mfcc(one[i].contiguous()).cpu().numpy()[0] for i in range(len(fr))])
         assert_mfcc_close(clip, g[f"mfcc{nf}"])
 
 

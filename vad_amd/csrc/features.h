@@ -51,6 +51,27 @@ __device__ __forceinline__ Feat3 feature_triple(float a0, float a1, float a2, fl
   return {mn, a3 - a1, (a4 - mn) - (mn - a0)};
 }
 
+// The same triple for kernels that flag NaN windows themselves (the wave
+// tile: a flagged window's features go to the MLP as 0 and its logits are
+// NaN): Mn without the NaN added in, and `bad` = flat coefficient or a NaN
+// Mn (an overflowed var times a zero / infinite e2) -- exactly the windows
+// whose feature_triple Mn is NaN, one select cheaper per item.
+__device__ __forceinline__ Feat3 feature_triple_flagged(float a0, float a1, float a2, float a3, float a4,
+                                                        int mode, bool& bad) {
+  if (mode != VAD_FEAT_ANALYSER) {
+    bad = false;
+    return {a2, a3 - a1, (a4 - a2) - (a2 - a0)};
+  }
+  const float sum = (((a0 + a1) + a2) + a3) + a4;
+  const float e0 = fmaf(sum, -0.2f, a0), e1 = fmaf(sum, -0.2f, a1), e2 = fmaf(sum, -0.2f, a2),
+              e3 = fmaf(sum, -0.2f, a3), e4 = fmaf(sum, -0.2f, a4);
+  const float var_s = fmaf(e4, e4, fmaf(e3, e3, fmaf(e2, e2, fmaf(e1, e1, e0 * e0)))) * (0.2f * 0x1p24f);
+  const bool flat = (a0 == a1) & (a1 == a2) & (a2 == a3) & (a3 == a4);
+  const float mn = fmaf(e2 * 0x1p12f, __builtin_amdgcn_rsqf(var_s), 0.f);
+  bad = flat | (mn != mn);
+  return {mn, a3 - a1, (a4 - mn) - (mn - a0)};
+}
+
 // Feature f (0 .. 3*mfcc_n-1) of the window whose 5 MFCC rows are r0..r4.
 __device__ __forceinline__ float window_feature(const float* __restrict__ r0,
                                                const float* __restrict__ r1,

@@ -7,6 +7,13 @@
 #include "vad_common.h"
 #include "features.h"
 
+#ifndef VAD_FEAT_FLAGGED
+#define VAD_FEAT_FLAGGED 1  // wave tile: flag NaN windows without adding the NaN in (one select less per item)
+#endif
+#ifndef VAD_FFN_MERGE0_SCALED
+#define VAD_FFN_MERGE0_SCALED 1  // merged layer 0: each lane forms only its own half (no select)
+#endif
+
 
 namespace vad {
 
@@ -312,6 +319,31 @@ __device__ __forceinline__ void split8(const float (&v)[8], h8& hi, h8& lo) {
   lo = __builtin_bit_cast(h8, lw);
 }
 
+// v - s f32(half SEL of hp), s = 0 or 1 (a VGPR): the merged first layer's
+// per-lane half (dense_h3 MERGE0)
+template <int SEL>
+__device__ __forceinline__ float sub_f16_half_scaled(float v, unsigned hp, float s) {
+  float d;
+  if constexpr (SEL == 0)
+    asm("v_fma_mix_f32 %0, -%1, %3, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hp), "v"(v), "v"(s));
+  else
+    asm("v_fma_mix_f32 %0, -%1, %3, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hp), "v"(v), "v"(s));
+  return d;
+}
+
+__device__ __forceinline__ void split8_merged(const float (&v)[8], h8& out, float s) {
+  u4 w;
+#pragma unroll
+  for (int q = 0; q < 8; q += 2) {
+    const f2 p = {v[q], v[q + 1]};
+    const h2 h = __builtin_convertvector(p, h2);
+    const unsigned hb = __builtin_bit_cast(unsigned, h);
+    const f2 d = {sub_f16_half_scaled<0>(v[q], hb, s), sub_f16_half_scaled<1>(v[q + 1], hb, s)};
+    w[q / 2] = __builtin_bit_cast(unsigned, __builtin_convertvector(d, h2));
+  }
+  out = __builtin_bit_cast(h8, w);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o));
@@ -387,8 +419,17 @@ __device__ __forceinline__ void dense_h3(FH A, FB b, float (&v)[KS][8], f32x4 (&
                                          bool bounded_rt = false) {
   const float sc = (BOUNDED || bounded_rt) ? 1.f : layer_scale<KS, NONNEG>(v);
   h8 bh[KS], bl[KS];
+  if constexpr (MERGE0 && VAD_FFN_MERGE0_SCALED) {
+    // lane groups g < 2 feed hi halves, g >= 2 lo halves: one split with the
+    // residual scaled by 0 / 1 per lane, f16(v - s f32(f16 v)), gives each
+    // lane its own half (s = 0: f16(v) bit for bit) without computing both
+    // and selecting
+    split8_merged(v[0], bh[0], (__builtin_amdgcn_workitem_id_x() & 63) >= 32 ? 1.f : 0.f);
+    bl[0] = bh[0];
+  } else {
 #pragma unroll
-  for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
+    for (int s = 0; s < KS; ++s) split8(v[s], bh[s], bl[s]);
+  }
   // MERGE0 (a first layer of <= 16 inputs, one K-step): lane group g < 2
   // feeds the hi halves of inputs 8 (g & 1) + q as k = 0..15, g >= 2 their lo
   // halves as k = 16..31, against A = [W_lo | 0] then [W_hi | W_hi] (the
@@ -606,6 +647,7 @@ struct LdsSlots {
 // ---------------------------------------------------------------------------
 constexpr int kWTile = 16;  // windows per wave tile
 
+
 // Lanes of one wave hand data to each other through LDS (rows -> features ->
 // operands).  A wave's LDS operations execute in order, so no wait is needed,
 // but in the language model each lane's accesses are independent and the
@@ -631,9 +673,15 @@ __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, 
     const int it = lane + 64 * r;
     if (r < kWTile * MN / 64 || it < kWTile * MN) {
       const int w = it / MN, c = it - MN * w;
+#if VAD_FEAT_FLAGGED
+      bool flat;
+      const Feat3 ft = feature_triple_flagged(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
+                                              R[it + 4 * MN], MODE, flat);
+#else
       const Feat3 ft = feature_triple(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
                                       R[it + 4 * MN], MODE);
       const bool flat = ft.mn != ft.mn;
+#endif
       if (flat) FL[w] = 1;
       float* xw = X + w * XS;
       xw[c] = flat ? 0.f : ft.mn;
