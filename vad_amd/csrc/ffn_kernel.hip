@@ -504,31 +504,16 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   // prefetch wait at the loop's back edge): offsets past the rows clamp to
   // the last float, so the last tile's unused windows see finite rows.  The
   // tile base is wave-uniform (a scalar address), the lane offsets 32-bit.
-#ifndef VAD_FFN_BUFFER_ROWS
-#define VAD_FFN_BUFFER_ROWS 1
-#endif
   auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
     const int64_t base = t * (kWTile * MN);
     const float* tb = mfcc + base;
     const int64_t rem = total - 1 - base;  // >= 0 for t < n_tiles
-#if VAD_FFN_BUFFER_ROWS
-    // a buffer resource per tile (scalar: base address and the bytes left,
-    // at most the tile's 260 floats): the hardware returns 0 past it, so the
-    // last tile's unused windows see finite rows with no per-lane clamp
-    // (one VGPR of lane offset, the 64-float steps as immediate offsets)
-    const int nrec = 4 * (int)(rem + 1 < kWRows ? rem + 1 : kWRows);
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(tb), (short)0, nrec, 0x00020000);
-#pragma unroll
-    for (int q = 0; q < kWRowRegs; ++q) dst[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * lane, 256 * q, 0);
-#else
     const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);  // byte offset clamp
 #pragma unroll
     for (int q = 0; q < kWRowRegs; ++q) {
       const unsigned ob = 4u * (unsigned)(lane + 64 * q);
       dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
     }
-#endif
   };
   // every fragment load done before the loop: the waitcnt pass would
   // otherwise leave counter waits for them in the loop body, where they
