@@ -605,6 +605,106 @@ __device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS
   dense_h3<T2, HP::K1, FB, true>(fh.at(HP::S0), fb + 4 * T1, v1, h2, true, IN_BOUNDED && h1_bounded);
 }
 
+// The hidden layers of a 13-64-64-2-shaped network (merged first layer,
+// bounded inputs, layer 1 under the host's bound) for TWO 16-window tiles at
+// once: every weight fragment read (from LDS) feeds both tiles' MFMAs, and
+// the two tiles' accumulator chains interleave.  Per tile the arithmetic is
+// dense_h3's, operation for operation: results bit-identical to two
+// mlp_hidden2_h3 calls.
+template <int KS0, int T1, int T2, class FB, class FH>
+__device__ __forceinline__ void mlp_hidden2_h3_pair(FH fh, FB fb, float (&xa)[1][8], float (&xb)[1][8],
+                                                    f32x4 (&ha)[T2], f32x4 (&hb)[T2]) {
+  using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
+  using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
+  static_assert(kMerge0<KS0> && HP::K0 == 1, "merged first layer");
+  constexpr int K1 = HP::K1;
+  const float s = (__builtin_amdgcn_workitem_id_x() & 63) >= 32 ? 1.f : 0.f;
+  auto relu4 = [](f32x4 o) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = o[r];
+      const int bits = __builtin_bit_cast(int, e);
+      o[r] = __builtin_bit_cast(float, bits > 0 ? bits : 0);
+    }
+    return o;
+  };
+  // layer 0: lo*hi, then hi*hi + hi*lo, each fragment on both tiles
+  h8 ba, bb;
+  split8_merged(xa[0], ba, s);
+  split8_merged(xb[0], bb, s);
+  f32x4 h1a[T1], h1b[T1];
+  {
+    f32x4 bias[T1];
+#pragma unroll
+    for (int mt = 0; mt < T1; ++mt) bias[mt] = (f32x4){fb[mt * 4 + 0], fb[mt * 4 + 1], fb[mt * 4 + 2], fb[mt * 4 + 3]};
+#pragma unroll
+    for (int mt = 0; mt < T1; ++mt) {
+      const h8 a1 = __builtin_bit_cast(h8, fh.get(mt, 1));
+      h1a[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ba, bias[mt], 0, 0, 0);
+      h1b[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bb, bias[mt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < T1; ++mt) {
+      const h8 a0 = __builtin_bit_cast(h8, fh.get(mt, 0));
+      h1a[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ba, h1a[mt], 0, 0, 0);
+      h1b[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bb, h1b[mt], 0, 0, 0);
+    }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int mt = 0; mt < T1; ++mt) {
+    h1a[mt] = relu4(h1a[mt]);
+    h1b[mt] = relu4(h1b[mt]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  // layer 1: lo*hi + hi*lo + hi*hi, small terms first, fragments shared
+  float va[K1][8], vb[K1][8];
+  acts_of<T1>(h1a, va);
+  acts_of<T1>(h1b, vb);
+  h8 bha[K1], bla[K1], bhb[K1], blb[K1];
+#pragma unroll
+  for (int k = 0; k < K1; ++k) {
+    split8(va[k], bha[k], bla[k]);
+    split8(vb[k], bhb[k], blb[k]);
+  }
+  const FH A = fh.at(HP::S0);
+  const FB b1 = fb + 4 * T1;
+  f32x4 bias[T2];
+#pragma unroll
+  for (int mt = 0; mt < T2; ++mt) bias[mt] = (f32x4){b1[mt * 4 + 0], b1[mt * 4 + 1], b1[mt * 4 + 2], b1[mt * 4 + 3]};
+#pragma unroll
+  for (int k = 0; k < K1; ++k)
+#pragma unroll
+    for (int mt = 0; mt < T2; ++mt) {
+      const h8 lo = __builtin_bit_cast(h8, A.get(mt * K1 + k, 1));
+      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bha[k], k == 0 ? bias[mt] : ha[mt], 0, 0, 0);
+      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bhb[k], k == 0 ? bias[mt] : hb[mt], 0, 0, 0);
+    }
+#pragma unroll
+  for (int k = 0; k < K1; ++k)
+#pragma unroll
+    for (int mt = 0; mt < T2; ++mt) {
+      const h8 hi = __builtin_bit_cast(h8, A.get(mt * K1 + k, 0));
+      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bla[k], ha[mt], 0, 0, 0);
+      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, blb[k], hb[mt], 0, 0, 0);
+    }
+#pragma unroll
+  for (int k = 0; k < K1; ++k)
+#pragma unroll
+    for (int mt = 0; mt < T2; ++mt) {
+      const h8 hi = __builtin_bit_cast(h8, A.get(mt * K1 + k, 0));
+      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bha[k], ha[mt], 0, 0, 0);
+      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bhb[k], hb[mt], 0, 0, 0);
+    }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int mt = 0; mt < T2; ++mt) {
+    ha[mt] = relu4(ha[mt]);
+    hb[mt] = relu4(hb[mt]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // Per-lane fragment slots read straight from global memory (L1 / L2
 // resident: the plan's tables are a few tens of KB), for kernels whose VGPRs
 // and LDS are taken by other work (the fused MFCC + FFN kernel).
@@ -662,24 +762,38 @@ __device__ __forceinline__ void wave_lds_handoff() { asm volatile("" ::: "memory
 // as 0 and stores 1 into its window's flag (after the wave's own zeroing
 // stores, in LDS order; a ds_or_b32 from all 13 coefficient lanes instead
 // serialises on the one address: +2.5 us per 1M windows).
-template <int IN, int XS, int MODE>
+// NT tiles at once (the pair kernel: NT = 2): their items run on one range
+// (NT * 208 items, ceil(NT * 208 / 64) rounds instead of NT * 4), tile k's
+// rows at R + k (208 + RGAP), its feature rows and flags right after tile
+// k - 1's (X + 16 k XS, FL + 16 k).
+template <int IN, int XS, int MODE, int NT = 1, int RGAP = 0>
 __device__ __forceinline__ void wave_tile_features(const float* __restrict__ R, float* __restrict__ X,
                                                    int* __restrict__ FL, int lane) {
   constexpr int MN = 13;
+  constexpr int NI = NT * kWTile * MN;  // items
   wave_lds_handoff();  // the rows R were stored by other lanes of this wave
-  if (lane < kWTile) FL[lane] = 0;
+  if (lane < NT * kWTile) FL[lane] = 0;
 #pragma unroll
-  for (int r = 0; r < (kWTile * MN + 63) / 64; ++r) {
+  for (int r = 0; r < (NI + 63) / 64; ++r) {
     const int it = lane + 64 * r;
-    if (r < kWTile * MN / 64 || it < kWTile * MN) {
+    if (r < NI / 64 || it < NI) {
       const int w = it / MN, c = it - MN * w;
+      // the row offset of tile it / 208 (compile-time outside the one round
+      // that straddles two tiles)
+      int ri = it;
+#pragma unroll
+      for (int k = 1; k < NT; ++k) {
+        constexpr int kTileItems = kWTile * MN;
+        if (64 * r >= k * kTileItems) ri += RGAP;
+        else if (64 * r + 63 >= k * kTileItems) ri += it >= k * kTileItems ? RGAP : 0;
+      }
 #if VAD_FEAT_FLAGGED
       bool flat;
-      const Feat3 ft = feature_triple_flagged(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
-                                              R[it + 4 * MN], MODE, flat);
+      const Feat3 ft = feature_triple_flagged(R[ri], R[ri + MN], R[ri + 2 * MN], R[ri + 3 * MN],
+                                              R[ri + 4 * MN], MODE, flat);
 #else
-      const Feat3 ft = feature_triple(R[it], R[it + MN], R[it + 2 * MN], R[it + 3 * MN],
-                                      R[it + 4 * MN], MODE);
+      const Feat3 ft = feature_triple(R[ri], R[ri + MN], R[ri + 2 * MN], R[ri + 3 * MN],
+                                      R[ri + 4 * MN], MODE);
       const bool flat = ft.mn != ft.mn;
 #endif
       if (flat) FL[w] = 1;

@@ -584,6 +584,141 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
   }
 }
 
+// ---------------------------------------------------------------------------
+// Tile pairs (13-64-64-2, labels only): the wave kernel above with each wave
+// taking TWO 16-window tiles per iteration (tiles t and t + n_waves): both
+// tiles' rows, features and operands as above, then the hidden layers of
+// both through mlp_hidden2_h3_pair (every LDS fragment read feeds two MFMAs,
+// the two chains interleave), the logit-difference label of each.  Labels
+// bit-identical to ffn_wave_kernel.  Feature rows at stride 20 (16 columns
+// read, conflict-free ds_read_b128): per wave 2 x (1,040 + 1,280) B of LDS.
+// VAD_FFN_PAIR selects it for the labels-only 13-64-64-2 launches.
+// ---------------------------------------------------------------------------
+#ifndef VAD_FFN_PAIR
+#define VAD_FFN_PAIR 1
+#endif
+#ifndef VAD_FFN_PAIR_FEAT
+#define VAD_FFN_PAIR_FEAT 1  // the pair's features over one item range (7 rounds, not 8)
+#endif
+#ifndef VAD_FFN_PAIR_WPS
+#define VAD_FFN_PAIR_WPS 3  // waves per SIMD the pair kernel is compiled for
+#endif
+template <int MODE>
+__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(VAD_FFN_PAIR_WPS))) void ffn_wave_pair_kernel(
+    FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
+  constexpr int KS0 = 4, T1 = 4, T2 = 4, NC = 2, MN = 13, IN = 13, XS = 20;
+  using TP = Topo<KS0, T1, T2, 1, 0, NC, false>;
+  using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
+  static_assert(TP::VL && TP::NL == 3, "VALU output layer");
+  __shared__ float rows_s[kWpb][2][kWRows];
+  __shared__ __attribute__((aligned(16))) float x_s[kWpb][2][kWTile * XS];
+  __shared__ int flat_s[kWpb][2][kWTile];
+  constexpr int NSL = TP::NB + TP::NV + TP::NVB;
+  constexpr int NSD = TP::TIL * 4 + 1;
+  constexpr int NSLP = (NSL + NSD + 3) & ~3;
+  __shared__ __attribute__((aligned(16))) float slot_s[4 * NSLP];
+  __shared__ u4 fh_s[HP::NS * 2 * 64];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4;
+  const int jw = lane & 15;
+  // the slot table (biases, output-layer weights, the class-1 minus class-0
+  // difference) and the split-f16 fragments, as in ffn_wave_kernel's kAll
+  {
+    auto slot_val = [&](int sl, int gg) {
+      const int src_sl = sl < TP::NB ? TP::NA_ALL + sl
+                                     : TP::NA_ALL + TP::NB + (sl - TP::NB < TP::NV ? sl - TP::NB
+                                                                                  : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
+      return net.frag[src_sl * 64 + 16 * gg];
+    };
+    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kWpb) {
+      const int gg = i / NSLP, sl = i - gg * NSLP;
+      float v = 0.f;
+      if (sl < NSL) {
+        v = slot_val(sl, gg);
+      } else if (sl < NSL + NSD) {
+        const int q = sl - NSL;
+        v = q < TP::TIL * 4 ? slot_val(TP::NB + TP::TIL * 4 + q, gg) - slot_val(TP::NB + q, gg)
+                            : slot_val(TP::NB + TP::NV + 1, gg) - slot_val(TP::NB + TP::NV, gg);
+      }
+      slot_s[i] = v;
+    }
+    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 64 * kWpb) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
+    __syncthreads();
+  }
+  const LdsRow fbs{slot_s + g * NSLP};
+  const LdsRow fvs{slot_s + g * NSLP + TP::NB};
+  const LdsRow fds{slot_s + g * NSLP + NSL};
+  const FragLds fh{fh_s, lane};
+  for (int k = 0; k < 2; ++k)
+    for (int i = lane; i < kWTile * XS; i += 64) x_s[wv][k][i] = 0.f;  // columns 13.. stay 0
+
+  const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
+  const int64_t total = (n_rows + 4) * MN;
+  const int64_t wave_id = (int64_t)blockIdx.x * kWpb + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * kWpb;
+  auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
+    const int64_t base = t * (kWTile * MN);
+    const float* tb = mfcc + base;
+    const int64_t rem = total - 1 - base;
+    const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);
+#pragma unroll
+    for (int q = 0; q < kWRowRegs; ++q) {
+      const unsigned ob = 4u * (unsigned)(lane + 64 * q);
+      dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
+    }
+  };
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0
+  // a pair = tiles t and t + n_waves (the second clamped to t past the end:
+  // computed, not stored)
+  auto second = [&](int64_t t) { return t + n_waves < n_tiles ? t + n_waves : t; };
+  float pre[2][kWRowRegs];
+  if (wave_id < n_tiles) {
+    load(wave_id, pre[0]);
+    load(second(wave_id), pre[1]);
+  }
+  for (int64_t t = wave_id; t < n_tiles; t += 2 * n_waves) {
+    const int64_t tb = second(t);
+    const int64_t tn = t + 2 * n_waves < n_tiles ? t + 2 * n_waves : t;
+    wave_lds_handoff();
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int q = 0; q < kWRowRegs; ++q)
+        if (lane + 64 * q < kWRows) rows_s[wv][k][lane + 64 * q] = pre[k][q];
+    load(tn, pre[0]);
+    load(second(tn), pre[1]);
+#if VAD_FFN_PAIR_FEAT
+    // both tiles' 416 items in 7 rounds (two calls: 8, the fourth of each a
+    // quarter full)
+    wave_tile_features<IN, XS, MODE, 2, kWRows - kWTile * MN>(rows_s[wv][0], x_s[wv][0], flat_s[wv][0], lane);
+#else
+    wave_tile_features<IN, XS, MODE>(rows_s[wv][0], x_s[wv][0], flat_s[wv][0], lane);
+    wave_tile_features<IN, XS, MODE>(rows_s[wv][1], x_s[wv][1], flat_s[wv][1], lane);
+#endif
+#if VAD_FFN_PRIO
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(VAD_FFN_PRIO);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    float xa[1][8], xb[1][8];
+    const int na = wave_tile_operands<1, IN, XS, false>(x_s[wv][0], flat_s[wv][0], lane, xa);
+    const int nb = wave_tile_operands<1, IN, XS, false>(x_s[wv][1], flat_s[wv][1], lane, xb);
+    f32x4 ha[T2], hb[T2];
+    mlp_hidden2_h3_pair<KS0, T1, T2>(fh, fbs, xa, xb, ha, hb);
+    const int la = valu_label2<TP, T2>(fds, fvs, ha, na);
+    const int lb = valu_label2<TP, T2>(fds, fvs, hb, nb);
+#if VAD_FFN_PRIO
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const int64_t wa = t * kWTile + jw, wb = tb * kWTile + jw;
+    if (g == 0 && wa < n_rows) labels[wa] = (uint8_t)la;
+    if (g == 0 && tb != t && wb < n_rows) labels[wb] = (uint8_t)lb;
+  }
+}
+
 // Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
 // window of each stream is its 5-slot MFCC ring in arrival order
 // (slot (count + d) % 5, oldest first); classify it if count >= 5, then push
@@ -691,6 +826,20 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
     constexpr bool kH3 = (KS0 == 10 && T1 == 4 && T2 == 2 && T3 == 1 && T4 == 1) ||
                          (KS0 == 4 && T1 == 4 && T2 == 4 && T3 == 1 && T4 == 0);
     if constexpr (kH3) {
+      if constexpr (KS0 == 4 && NC <= 2) {
+        // tile pairs: labels-only analyser launches whose layer-1 inputs the
+        // host proved f16-bounded (the single-tile kernel keeps the rescale)
+        if (VAD_FFN_PAIR && mfcc_n == 13 && net.fragh && !net.logits && net.h1_bounded &&
+            mode == VAD_FEAT_ANALYSER && net.n_classes == 2) {
+          const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
+          int64_t pblocks = ((n_tiles + 1) / 2 + kWpb - 1) / kWpb;
+          const int64_t pcap = VAD_FFN_PAIR_WPS * 4 / kWpb * ffn_num_cus();
+          if (pblocks > pcap) pblocks = pcap;
+          hipLaunchKernelGGL((ffn_wave_pair_kernel<VAD_FEAT_ANALYSER>), dim3((int)pblocks), dim3(64 * kWpb), 0, st,
+                             net, in, n_rows, labels);
+          return hipGetLastError();
+        }
+      }
       if (mfcc_n == 13 && net.fragh && VAD_FFN_WAVE) {
         // one resident wave per SIMD pair slot: 2 blocks of 4 waves per CU
         int64_t wblocks = (n_rows + kWpb * kWTile - 1) / (kWpb * kWTile);
