@@ -606,14 +606,13 @@ __device__ __forceinline__ void mlp_hidden2_h3(FH fh, FB fb, float (&x0)[(4 * KS
 }
 
 // The hidden layers of a 13-64-64-2-shaped network (merged first layer,
-// bounded inputs, layer 1 under the host's bound) for TWO 16-window tiles at
-// once: every weight fragment read (from LDS) feeds both tiles' MFMAs, and
-// the two tiles' accumulator chains interleave.  Per tile the arithmetic is
-// dense_h3's, operation for operation: results bit-identical to two
-// mlp_hidden2_h3 calls.
-template <int KS0, int T1, int T2, class FB, class FH>
-__device__ __forceinline__ void mlp_hidden2_h3_pair(FH fh, FB fb, float (&xa)[1][8], float (&xb)[1][8],
-                                                    f32x4 (&ha)[T2], f32x4 (&hb)[T2]) {
+// bounded inputs, layer 1 under the host's bound) for NT 16-window tiles at
+// once (the tile-group kernel): every weight fragment read (from LDS) feeds
+// the NT tiles' MFMAs, and their accumulator chains interleave.  Per tile
+// the arithmetic is dense_h3's, operation for operation: results
+// bit-identical to NT mlp_hidden2_h3 calls.
+template <int KS0, int T1, int T2, int NT, class FB, class FH>
+__device__ __forceinline__ void mlp_hidden2_h3_multi(FH fh, FB fb, float (&x)[NT][1][8], f32x4 (&h)[NT][T2]) {
   using TP = Topo<KS0, T1, T2, 1, 0, 2, false>;
   using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
   static_assert(kMerge0<KS0> && HP::K0 == 1, "merged first layer");
@@ -628,11 +627,11 @@ __device__ __forceinline__ void mlp_hidden2_h3_pair(FH fh, FB fb, float (&xa)[1]
     }
     return o;
   };
-  // layer 0: lo*hi, then hi*hi + hi*lo, each fragment on both tiles
-  h8 ba, bb;
-  split8_merged(xa[0], ba, s);
-  split8_merged(xb[0], bb, s);
-  f32x4 h1a[T1], h1b[T1];
+  // layer 0: lo*hi, then hi*hi + hi*lo, each fragment on every tile
+  h8 b0[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) split8_merged(x[t][0], b0[t], s);
+  f32x4 h1[NT][T1];
   {
     f32x4 bias[T1];
 #pragma unroll
@@ -640,32 +639,30 @@ __device__ __forceinline__ void mlp_hidden2_h3_pair(FH fh, FB fb, float (&xa)[1]
 #pragma unroll
     for (int mt = 0; mt < T1; ++mt) {
       const h8 a1 = __builtin_bit_cast(h8, fh.get(mt, 1));
-      h1a[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, ba, bias[mt], 0, 0, 0);
-      h1b[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, bb, bias[mt], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b0[t], bias[mt], 0, 0, 0);
     }
 #pragma unroll
     for (int mt = 0; mt < T1; ++mt) {
       const h8 a0 = __builtin_bit_cast(h8, fh.get(mt, 0));
-      h1a[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, ba, h1a[mt], 0, 0, 0);
-      h1b[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, bb, h1b[mt], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h1[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b0[t], h1[t][mt], 0, 0, 0);
     }
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int mt = 0; mt < T1; ++mt) {
-    h1a[mt] = relu4(h1a[mt]);
-    h1b[mt] = relu4(h1b[mt]);
-  }
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int mt = 0; mt < T1; ++mt) h1[t][mt] = relu4(h1[t][mt]);
   __builtin_amdgcn_sched_barrier(0);
   // layer 1: lo*hi + hi*lo + hi*hi, small terms first, fragments shared
-  float va[K1][8], vb[K1][8];
-  acts_of<T1>(h1a, va);
-  acts_of<T1>(h1b, vb);
-  h8 bha[K1], bla[K1], bhb[K1], blb[K1];
+  h8 bh[NT][K1], bl[NT][K1];
 #pragma unroll
-  for (int k = 0; k < K1; ++k) {
-    split8(va[k], bha[k], bla[k]);
-    split8(vb[k], bhb[k], blb[k]);
+  for (int t = 0; t < NT; ++t) {
+    float v[K1][8];
+    acts_of<T1>(h1[t], v);
+#pragma unroll
+    for (int k = 0; k < K1; ++k) split8(v[k], bh[t][k], bl[t][k]);
   }
   const FH A = fh.at(HP::S0);
   const FB b1 = fb + 4 * T1;
@@ -677,31 +674,31 @@ __device__ __forceinline__ void mlp_hidden2_h3_pair(FH fh, FB fb, float (&xa)[1]
 #pragma unroll
     for (int mt = 0; mt < T2; ++mt) {
       const h8 lo = __builtin_bit_cast(h8, A.get(mt * K1 + k, 1));
-      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bha[k], k == 0 ? bias[mt] : ha[mt], 0, 0, 0);
-      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bhb[k], k == 0 ? bias[mt] : hb[mt], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo, bh[t][k], k == 0 ? bias[mt] : h[t][mt], 0, 0, 0);
     }
 #pragma unroll
   for (int k = 0; k < K1; ++k)
 #pragma unroll
     for (int mt = 0; mt < T2; ++mt) {
       const h8 hi = __builtin_bit_cast(h8, A.get(mt * K1 + k, 0));
-      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bla[k], ha[mt], 0, 0, 0);
-      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, blb[k], hb[mt], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bl[t][k], h[t][mt], 0, 0, 0);
     }
 #pragma unroll
   for (int k = 0; k < K1; ++k)
 #pragma unroll
     for (int mt = 0; mt < T2; ++mt) {
       const h8 hi = __builtin_bit_cast(h8, A.get(mt * K1 + k, 0));
-      ha[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bha[k], ha[mt], 0, 0, 0);
-      hb[mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bhb[k], hb[mt], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bh[t][k], h[t][mt], 0, 0, 0);
     }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-  for (int mt = 0; mt < T2; ++mt) {
-    ha[mt] = relu4(ha[mt]);
-    hb[mt] = relu4(hb[mt]);
-  }
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int mt = 0; mt < T2; ++mt) h[t][mt] = relu4(h[t][mt]);
   __builtin_amdgcn_sched_barrier(0);
 }
 

@@ -585,34 +585,33 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
 }
 
 // ---------------------------------------------------------------------------
-// Tile pairs (13-64-64-2, labels only): the wave kernel above with each wave
-// taking TWO 16-window tiles per iteration (tiles t and t + n_waves): both
-// tiles' rows, features and operands as above, then the hidden layers of
-// both through mlp_hidden2_h3_pair (every LDS fragment read feeds two MFMAs,
-// the two chains interleave), the logit-difference label of each.  Labels
-// bit-identical to ffn_wave_kernel.  Feature rows at stride 20 (16 columns
-// read, conflict-free ds_read_b128): per wave 2 x (1,040 + 1,280) B of LDS.
-// VAD_FFN_PAIR selects it for the labels-only 13-64-64-2 launches.
+// Tile groups (13-64-64-2, labels only): the wave kernel above with each
+// wave taking NT 16-window tiles per iteration (tiles t, t + n_waves, ...):
+// the NT tiles' rows, their features over one item range (NT x 208 items:
+// 7 rounds for a pair where two single tiles take 8), their operands, then
+// the hidden layers of all NT through mlp_hidden2_h3_multi (every LDS
+// fragment read feeds NT MFMAs, the NT chains interleave) and the logit-
+// difference label of each.  Labels bit-identical to ffn_wave_kernel.
+// Feature rows at stride 20 (16 columns read, conflict-free ds_read_b128):
+// per wave NT x (1,040 + 1,280) B of LDS.  VAD_FFN_GROUP = NT (0: off) for
+// the labels-only analyser launches of 13-64-64-2.
 // ---------------------------------------------------------------------------
-#ifndef VAD_FFN_PAIR
-#define VAD_FFN_PAIR 1
+#ifndef VAD_FFN_GROUP
+#define VAD_FFN_GROUP 2
 #endif
-#ifndef VAD_FFN_PAIR_FEAT
-#define VAD_FFN_PAIR_FEAT 1  // the pair's features over one item range (7 rounds, not 8)
-#endif
-#ifndef VAD_FFN_PAIR_WPS
-#define VAD_FFN_PAIR_WPS 3  // waves per SIMD the pair kernel is compiled for
-#endif
-template <int MODE>
-__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(VAD_FFN_PAIR_WPS))) void ffn_wave_pair_kernel(
+// waves per SIMD each group size fits: 168 VGPRs for a pair, 2 beyond
+template <int NT>
+constexpr int kGroupWps = NT <= 2 ? 3 : 2;
+template <int MODE, int NT>
+__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kGroupWps<NT>))) void ffn_wave_group_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
   constexpr int KS0 = 4, T1 = 4, T2 = 4, NC = 2, MN = 13, IN = 13, XS = 20;
   using TP = Topo<KS0, T1, T2, 1, 0, NC, false>;
   using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
   static_assert(TP::VL && TP::NL == 3, "VALU output layer");
-  __shared__ float rows_s[kWpb][2][kWRows];
-  __shared__ __attribute__((aligned(16))) float x_s[kWpb][2][kWTile * XS];
-  __shared__ int flat_s[kWpb][2][kWTile];
+  __shared__ float rows_s[kWpb][NT][kWRows];
+  __shared__ __attribute__((aligned(16))) float x_s[kWpb][NT][kWTile * XS];
+  __shared__ int flat_s[kWpb][NT][kWTile];
   constexpr int NSL = TP::NB + TP::NV + TP::NVB;
   constexpr int NSD = TP::TIL * 4 + 1;
   constexpr int NSLP = (NSL + NSD + 3) & ~3;
@@ -650,7 +649,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(VAD_F
   const LdsRow fvs{slot_s + g * NSLP + TP::NB};
   const LdsRow fds{slot_s + g * NSLP + NSL};
   const FragLds fh{fh_s, lane};
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < NT; ++k)
     for (int i = lane; i < kWTile * XS; i += 64) x_s[wv][k][i] = 0.f;  // columns 13.. stay 0
 
   const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
@@ -669,53 +668,50 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(VAD_F
     }
   };
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0
-  // a pair = tiles t and t + n_waves (the second clamped to t past the end:
+  // tile k of the group at t: t + k n_waves (clamped to t past the end:
   // computed, not stored)
-  auto second = [&](int64_t t) { return t + n_waves < n_tiles ? t + n_waves : t; };
-  float pre[2][kWRowRegs];
+  auto member = [&](int64_t t, int k) { return t + k * n_waves < n_tiles ? t + k * n_waves : t; };
+  float pre[NT][kWRowRegs];
   if (wave_id < n_tiles) {
-    load(wave_id, pre[0]);
-    load(second(wave_id), pre[1]);
+#pragma unroll
+    for (int k = 0; k < NT; ++k) load(member(wave_id, k), pre[k]);
   }
-  for (int64_t t = wave_id; t < n_tiles; t += 2 * n_waves) {
-    const int64_t tb = second(t);
-    const int64_t tn = t + 2 * n_waves < n_tiles ? t + 2 * n_waves : t;
+  for (int64_t t = wave_id; t < n_tiles; t += NT * n_waves) {
+    const int64_t tn = t + NT * n_waves < n_tiles ? t + NT * n_waves : t;
     wave_lds_handoff();
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < NT; ++k)
 #pragma unroll
       for (int q = 0; q < kWRowRegs; ++q)
         if (lane + 64 * q < kWRows) rows_s[wv][k][lane + 64 * q] = pre[k][q];
-    load(tn, pre[0]);
-    load(second(tn), pre[1]);
-#if VAD_FFN_PAIR_FEAT
-    // both tiles' 416 items in 7 rounds (two calls: 8, the fourth of each a
-    // quarter full)
-    wave_tile_features<IN, XS, MODE, 2, kWRows - kWTile * MN>(rows_s[wv][0], x_s[wv][0], flat_s[wv][0], lane);
-#else
-    wave_tile_features<IN, XS, MODE>(rows_s[wv][0], x_s[wv][0], flat_s[wv][0], lane);
-    wave_tile_features<IN, XS, MODE>(rows_s[wv][1], x_s[wv][1], flat_s[wv][1], lane);
-#endif
+#pragma unroll
+    for (int k = 0; k < NT; ++k) load(member(tn, k), pre[k]);
+    wave_tile_features<IN, XS, MODE, NT, kWRows - kWTile * MN>(rows_s[wv][0], x_s[wv][0], flat_s[wv][0], lane);
 #if VAD_FFN_PRIO
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(VAD_FFN_PRIO);
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    float xa[1][8], xb[1][8];
-    const int na = wave_tile_operands<1, IN, XS, false>(x_s[wv][0], flat_s[wv][0], lane, xa);
-    const int nb = wave_tile_operands<1, IN, XS, false>(x_s[wv][1], flat_s[wv][1], lane, xb);
-    f32x4 ha[T2], hb[T2];
-    mlp_hidden2_h3_pair<KS0, T1, T2>(fh, fbs, xa, xb, ha, hb);
-    const int la = valu_label2<TP, T2>(fds, fvs, ha, na);
-    const int lb = valu_label2<TP, T2>(fds, fvs, hb, nb);
+    float x[NT][1][8];
+    int fl[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) fl[k] = wave_tile_operands<1, IN, XS, false>(x_s[wv][k], flat_s[wv][k], lane, x[k]);
+    f32x4 h[NT][T2];
+    mlp_hidden2_h3_multi<KS0, T1, T2, NT>(fh, fbs, x, h);
+    int lab[NT];
+#pragma unroll
+    for (int k = 0; k < NT; ++k) lab[k] = valu_label2<TP, T2>(fds, fvs, h[k], fl[k]);
 #if VAD_FFN_PRIO
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 #endif
-    const int64_t wa = t * kWTile + jw, wb = tb * kWTile + jw;
-    if (g == 0 && wa < n_rows) labels[wa] = (uint8_t)la;
-    if (g == 0 && tb != t && wb < n_rows) labels[wb] = (uint8_t)lb;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      const int64_t tk = member(t, k);
+      const int64_t w = tk * kWTile + jw;
+      if (g == 0 && (k == 0 || tk != t) && w < n_rows) labels[w] = (uint8_t)lab[k];
+    }
   }
 }
 
@@ -827,15 +823,16 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
                          (KS0 == 4 && T1 == 4 && T2 == 4 && T3 == 1 && T4 == 0);
     if constexpr (kH3) {
       if constexpr (KS0 == 4 && NC <= 2) {
-        // tile pairs: labels-only analyser launches whose layer-1 inputs the
+        // tile groups: labels-only analyser launches whose layer-1 inputs the
         // host proved f16-bounded (the single-tile kernel keeps the rescale)
-        if (VAD_FFN_PAIR && mfcc_n == 13 && net.fragh && !net.logits && net.h1_bounded &&
+        if (VAD_FFN_GROUP >= 2 && mfcc_n == 13 && net.fragh && !net.logits && net.h1_bounded &&
             mode == VAD_FEAT_ANALYSER && net.n_classes == 2) {
+          constexpr int NT = VAD_FFN_GROUP >= 2 ? VAD_FFN_GROUP : 2;
           const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
-          int64_t pblocks = ((n_tiles + 1) / 2 + kWpb - 1) / kWpb;
-          const int64_t pcap = VAD_FFN_PAIR_WPS * 4 / kWpb * ffn_num_cus();
-          if (pblocks > pcap) pblocks = pcap;
-          hipLaunchKernelGGL((ffn_wave_pair_kernel<VAD_FEAT_ANALYSER>), dim3((int)pblocks), dim3(64 * kWpb), 0, st,
+          int64_t gblocks = ((n_tiles + NT - 1) / NT + kWpb - 1) / kWpb;
+          const int64_t gcap = kGroupWps<NT> * 4 / kWpb * ffn_num_cus();
+          if (gblocks > gcap) gblocks = gcap;
+          hipLaunchKernelGGL((ffn_wave_group_kernel<VAD_FEAT_ANALYSER, NT>), dim3((int)gblocks), dim3(64 * kWpb), 0, st,
                              net, in, n_rows, labels);
           return hipGetLastError();
         }
