@@ -13,6 +13,9 @@
 #ifndef VAD_FFN_MERGE0_SCALED
 #define VAD_FFN_MERGE0_SCALED 1  // merged layer 0: each lane forms only its own half (no select)
 #endif
+#ifndef VAD_FFN_L1_MTMAJOR
+#define VAD_FFN_L1_MTMAJOR 1  // tile groups' layer 1 one output tile at a time (its fragments only live)
+#endif
 
 
 namespace vad {
@@ -669,6 +672,33 @@ __device__ __forceinline__ void mlp_hidden2_h3_multi(FH fh, FB fb, float (&x)[NT
   f32x4 bias[T2];
 #pragma unroll
   for (int mt = 0; mt < T2; ++mt) bias[mt] = (f32x4){b1[mt * 4 + 0], b1[mt * 4 + 1], b1[mt * 4 + 2], b1[mt * 4 + 3]};
+#if VAD_FFN_L1_MTMAJOR
+  // one output tile mt at a time (its K1 lo and K1 hi fragments live, not
+  // the layer's 2 T2 K1): each accumulator's products in the same order as
+  // below, so the results are identical
+#pragma unroll
+  for (int mt = 0; mt < T2; ++mt) {
+    h8 lo[K1], hi[K1];
+#pragma unroll
+    for (int k = 0; k < K1; ++k) {
+      lo[k] = __builtin_bit_cast(h8, A.get(mt * K1 + k, 1));
+      hi[k] = __builtin_bit_cast(h8, A.get(mt * K1 + k, 0));
+    }
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(lo[k], bh[t][k], k == 0 ? bias[mt] : h[t][mt], 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi[k], bl[t][k], h[t][mt], 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < K1; ++k)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi[k], bh[t][k], h[t][mt], 0, 0, 0);
+  }
+#else
 #pragma unroll
   for (int k = 0; k < K1; ++k)
 #pragma unroll
@@ -694,6 +724,7 @@ __device__ __forceinline__ void mlp_hidden2_h3_multi(FH fh, FB fb, float (&x)[NT
 #pragma unroll
       for (int t = 0; t < NT; ++t) h[t][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(hi, bh[t][k], h[t][mt], 0, 0, 0);
     }
+#endif
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < NT; ++t)

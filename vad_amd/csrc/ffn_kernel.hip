@@ -599,19 +599,28 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(WaveR
 #ifndef VAD_FFN_GROUP
 #define VAD_FFN_GROUP 2
 #endif
-// waves per SIMD each group size fits: 168 VGPRs for a pair, 2 beyond
+// waves per SIMD each group size fits: a pair 120 VGPRs (layer 1 one output
+// tile at a time, VAD_FFN_L1_MTMAJOR) and 64.1 KB of LDS per 8-wave block
+// (two blocks per CU): 4; larger groups 2
+#ifndef VAD_FFN_GROUP_WPS
+#define VAD_FFN_GROUP_WPS 0  // 0: by group size
+#endif
 template <int NT>
-constexpr int kGroupWps = NT <= 2 ? 3 : 2;
+constexpr int kGroupWps = VAD_FFN_GROUP_WPS ? VAD_FFN_GROUP_WPS : NT <= 2 ? 4 : 2;
+#ifndef VAD_FFN_GROUP_WPB
+#define VAD_FFN_GROUP_WPB 8  // waves per block (sharing the block's LDS fragments)
+#endif
+constexpr int kGWpb = VAD_FFN_GROUP_WPB;
 template <int MODE, int NT>
-__global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kGroupWps<NT>))) void ffn_wave_group_kernel(
+__global__ __launch_bounds__(64 * kGWpb) __attribute__((amdgpu_waves_per_eu(kGroupWps<NT>))) void ffn_wave_group_kernel(
     FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
   constexpr int KS0 = 4, T1 = 4, T2 = 4, NC = 2, MN = 13, IN = 13, XS = 20;
   using TP = Topo<KS0, T1, T2, 1, 0, NC, false>;
   using HP = HTopo<TP, KS0, T1, T2, 1, 0>;
   static_assert(TP::VL && TP::NL == 3, "VALU output layer");
-  __shared__ float rows_s[kWpb][NT][kWRows];
-  __shared__ __attribute__((aligned(16))) float x_s[kWpb][NT][kWTile * XS];
-  __shared__ int flat_s[kWpb][NT][kWTile];
+  __shared__ float rows_s[kGWpb][NT][kWRows];
+  __shared__ __attribute__((aligned(16))) float x_s[kGWpb][NT][kWTile * XS];
+  __shared__ int flat_s[kGWpb][NT][kWTile];
   constexpr int NSL = TP::NB + TP::NV + TP::NVB;
   constexpr int NSD = TP::TIL * 4 + 1;
   constexpr int NSLP = (NSL + NSD + 3) & ~3;
@@ -630,7 +639,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kGrou
                                                                                   : 4 * TP::TIL * 4 + sl - TP::NB - TP::NV);
       return net.frag[src_sl * 64 + 16 * gg];
     };
-    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kWpb) {
+    for (int i = threadIdx.x; i < 4 * NSLP; i += 64 * kGWpb) {
       const int gg = i / NSLP, sl = i - gg * NSLP;
       float v = 0.f;
       if (sl < NSL) {
@@ -642,7 +651,7 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kGrou
       }
       slot_s[i] = v;
     }
-    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 64 * kWpb) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
+    for (int i = threadIdx.x; i < HP::NS * 2 * 64; i += 64 * kGWpb) fh_s[i] = reinterpret_cast<const u4*>(net.fragh)[i];
     __syncthreads();
   }
   const LdsRow fbs{slot_s + g * NSLP};
@@ -654,8 +663,8 @@ __global__ __launch_bounds__(64 * kWpb) __attribute__((amdgpu_waves_per_eu(kGrou
 
   const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
   const int64_t total = (n_rows + 4) * MN;
-  const int64_t wave_id = (int64_t)blockIdx.x * kWpb + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * kWpb;
+  const int64_t wave_id = (int64_t)blockIdx.x * kGWpb + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * kGWpb;
   auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
     const int64_t base = t * (kWTile * MN);
     const float* tb = mfcc + base;
@@ -829,10 +838,10 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
             mode == VAD_FEAT_ANALYSER && net.n_classes == 2) {
           constexpr int NT = VAD_FFN_GROUP >= 2 ? VAD_FFN_GROUP : 2;
           const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
-          int64_t gblocks = ((n_tiles + NT - 1) / NT + kWpb - 1) / kWpb;
-          const int64_t gcap = kGroupWps<NT> * 4 / kWpb * ffn_num_cus();
+          int64_t gblocks = ((n_tiles + NT - 1) / NT + kGWpb - 1) / kGWpb;
+          const int64_t gcap = kGroupWps<NT> * 4 / kGWpb * ffn_num_cus();
           if (gblocks > gcap) gblocks = gcap;
-          hipLaunchKernelGGL((ffn_wave_group_kernel<VAD_FEAT_ANALYSER, NT>), dim3((int)gblocks), dim3(64 * kWpb), 0, st,
+          hipLaunchKernelGGL((ffn_wave_group_kernel<VAD_FEAT_ANALYSER, NT>), dim3((int)gblocks), dim3(64 * kGWpb), 0, st,
                              net, in, n_rows, labels);
           return hipGetLastError();
         }
