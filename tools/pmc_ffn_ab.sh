@@ -14,4 +14,5 @@ for v in "$@"; do
       --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu > $OUT/$v.p$i.log 2>&1 || { tail -20 $OUT/$v.p$i.log; exit 1; }
   done < tools/pmc_ffn.txt
 done
-python3 tools/pmc_ffn_report.py $OUT "$@"
+python3 tools/pmc_ffn_report.py $OUT "$@" > $OUT/report.json && cat $OUT/report.json
+for v in "$@"; do rm -rf $OUT/$v; done  # the raw counter CSVs exceed what gpurun copies back
