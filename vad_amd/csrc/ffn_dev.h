@@ -746,27 +746,6 @@ struct FragGlobal {
   __device__ u4 get(int sl, int h) const { return p[(2 * sl + h) * 64 + lane]; }
   __device__ FragGlobal at(int off) const { return {p + 2 * off * 64, lane}; }
 };
-// The same fragments through a buffer resource: one per-lane offset VGPR
-// (lane x 16 B) for every slot, the slot's offset in an SGPR -- no per-slot
-// 64-bit address registers (a kernel with 80 VGPRs cannot hold 24 of them)
-struct FragBuf {
-  __amdgpu_buffer_rsrc_t r;
-  int voff;  // lane * 16
-  int base;  // slot offset of this accessor (compile-time after inlining)
-  __device__ u4 get(int sl, int h) const {
-    return __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, (2 * (base + sl) + h) * 1024, 0));
-  }
-  __device__ FragBuf at(int off) const { return {r, voff, base + off}; }
-};
-// VluSlots through a buffer resource (the same slot order; voff = lane * 4)
-template <int NV, int TIL4>
-struct VluBuf {
-  __amdgpu_buffer_rsrc_t r;
-  int voff;
-  __device__ float operator[](int i) const {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, (i < NV ? i : 4 * TIL4 + i - NV) * 256, 0));
-  }
-};
 struct LaneSlots {
   const float* p;  // frag + b0 * 64 + lane
   __device__ float operator[](int s) const { return p[s * 64]; }

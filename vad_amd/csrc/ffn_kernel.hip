@@ -724,127 +724,6 @@ __global__ __launch_bounds__(64 * kGWpb) __attribute__((amdgpu_waves_per_eu(kGro
   }
 }
 
-// ---------------------------------------------------------------------------
-// The lean window kernel (13-64-64-2, analyser, labels only): sized to run
-// BESIDE the MFCC kernel on the same CUs -- a pipeline's FFN of clip k next
-// to the MFCC of clip k + 1 on another stream.  The MFCC workgroup holds
-// 2 x 216 VGPRs per SIMD and 157,696 B of LDS per CU, so this kernel's block
-// is one wave per SIMD within the 80 VGPRs left, and ~5 KB of LDS: the
-// tile's 20 MFCC rows per wave and a compact bias / label-weight table.  The
-// split-f16 fragments come from global memory (24 KB, L2-resident), the
-// layer-0 operands are formed in registers: lane (g, j) computes coefficients
-// 8 (g & 1) + 4 (g >> 1) + i (i < 4) of window j, and one v_permlane32_swap
-// per register gives every lane the 8 inputs of its lane group (lanes g and
-// g ^ 2 hold the two halves of the same 8) -- no LDS feature tile.  Same
-// arithmetic as ffn_wave_group_kernel operation for operation: labels
-// bit-identical.
-// ---------------------------------------------------------------------------
-#ifndef VAD_FFN_LEAN
-#define VAD_FFN_LEAN 0
-#endif
-constexpr int kLeanSlots = 52;  // per lane group: 16 + 16 biases, 16 + 1 differences, pad
-template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void ffn_lean_kernel(
-    FfnDev net, const float* __restrict__ mfcc, int64_t n_rows, uint8_t* __restrict__ labels) {
-  constexpr int KS0 = 4, T1 = 4, T2 = 4, NC = 2, MN = 13;
-  using TP = Topo<KS0, T1, T2, 1, 0, NC, false>;
-  static_assert(TP::VL && TP::NL == 3 && TP::TIL == 4, "VALU output layer");
-  __shared__ float rows_s[4][kWRows];
-  __shared__ __attribute__((aligned(16))) float slot_s[4 * kLeanSlots];
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = lane >> 4;
-  const int jw = lane & 15;
-  {
-    auto slot_val = [&](int sl, int gg) { return net.frag[(TP::NA_ALL + sl) * 64 + 16 * gg]; };
-    for (int i = threadIdx.x; i < 4 * kLeanSlots; i += 256) {
-      const int gg = i / kLeanSlots, sl = i - gg * kLeanSlots;
-      float v = 0.f;
-      if (sl < 4 * (T1 + T2)) v = slot_val(sl, gg);  // the two hidden layers' biases
-      else if (sl < 4 * (T1 + T2) + TP::TIL * 4) {   // class 1 minus class 0 weights
-        const int q = sl - 4 * (T1 + T2);
-        v = slot_val(TP::NB + TP::TIL * 4 + q, gg) - slot_val(TP::NB + q, gg);
-      } else if (sl == 4 * (T1 + T2) + TP::TIL * 4) {  // and biases
-        v = slot_val(TP::NB + 4 * TP::TIL * 4 + 1, gg) - slot_val(TP::NB + 4 * TP::TIL * 4, gg);
-      }
-      slot_s[i] = v;
-    }
-    __syncthreads();
-  }
-  const LdsRow fbs{slot_s + g * kLeanSlots};
-  const LdsRow fds{slot_s + g * kLeanSlots + 4 * (T1 + T2)};
-  // the VALU output layer's own slots, for valu_label2's rare two-logit rerun
-  const VluBuf<TP::NV, TP::TIL * 4> fvs{
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(net.frag) + (TP::NA_ALL + TP::NB) * 64, 0,
-                                        (4 * TP::TIL * 4 + NC) * 256, 0x00020000),
-      lane * 4};
-  // raw buffer over the plan's fragments (gfx9 dword 3: 32-bit elements,
-  // no swizzle); every slot offset is below the record count
-  const FragBuf fh{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(net.fragh), 0,
-                                                     HTopo<TP, KS0, T1, T2, 1, 0>::NS * 2 * 1024, 0x00020000),
-                   lane * 16, 0};
-  float* R = rows_s[wv];
-
-  const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
-  const int64_t total = (n_rows + 4) * MN;
-  const int64_t wave_id = (int64_t)blockIdx.x * 4 + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * 4;
-  auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
-    const int64_t base = t * (kWTile * MN);
-    const float* tb = mfcc + base;
-    const int64_t rem = total - 1 - base;
-    const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);
-#pragma unroll
-    for (int q = 0; q < kWRowRegs; ++q) {
-      const unsigned ob = 4u * (unsigned)(lane + 64 * q);
-      dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
-    }
-  };
-  // coefficient block of this lane: 0..3 (g 0), 8..11 (g 1), 4..7 (g 2), 12..15 (g 3)
-  const int cb = 8 * (g & 1) + 4 * (g >> 1);
-  float pre[kWRowRegs];
-  if (wave_id < n_tiles) load(wave_id, pre);
-  for (int64_t t = wave_id; t < n_tiles; t += n_waves) {
-    const int64_t tn = t + n_waves < n_tiles ? t + n_waves : t;
-    wave_lds_handoff();
-#pragma unroll
-    for (int q = 0; q < kWRowRegs; ++q)
-      if (lane + 64 * q < kWRows) R[lane + 64 * q] = pre[q];
-    load(tn, pre);
-    wave_lds_handoff();
-    // features of (window jw, coefficient cb + i); coefficients 13..15 (lane
-    // group 3, i >= 1) read the next row's first values and are dropped
-    float f[4];
-    bool flat = false;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ri = jw * MN + cb + i;
-      bool bad;
-      const Feat3 ft = feature_triple_flagged(R[ri], R[ri + MN], R[ri + 2 * MN], R[ri + 3 * MN], R[ri + 4 * MN],
-                                              MODE, bad);
-      if (i > 0) bad = bad && g != 3;
-      flat |= bad;
-      f[i] = (bad || (i > 0 && g == 3)) ? 0.f : ft.mn;
-    }
-    const int wnan = lane_or_xor48(flat ? 1 : 0);
-    // lanes g and g ^ 2 exchange their four: x = [own | partner] in rows
-    // 0-1, [partner | own] in rows 2-3 -- inputs 8 (g & 1) + q either way
-    float x[1][1][8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float a = f[i], b = f[i];
-      asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-      x[0][0][i] = a;
-      x[0][0][4 + i] = b;
-    }
-    f32x4 h[1][T2];
-    mlp_hidden2_h3_multi<KS0, T1, T2, 1>(fh, fbs, x, h);
-    const int lab = valu_label2<TP, T2>(fds, fvs, h[0], wnan);
-    const int64_t w = t * kWTile + jw;
-    if (g == 0 && w < n_rows) labels[w] = (uint8_t)lab;
-  }
-}
-
 // Streaming step for S analyser streams (sklearn_analyser.py:46-82): the
 // window of each stream is its 5-slot MFCC ring in arrival order
 // (slot (count + d) % 5, oldest first); classify it if count >= 5, then push
@@ -955,15 +834,6 @@ static hipError_t launch_topo(const FfnDev& net, int src, const float* in, int64
       if constexpr (KS0 == 4 && NC <= 2) {
         // tile groups: labels-only analyser launches whose layer-1 inputs the
         // host proved f16-bounded (the single-tile kernel keeps the rescale)
-        if (VAD_FFN_LEAN && mfcc_n == 13 && net.fragh && !net.logits && net.h1_bounded &&
-            mode == VAD_FEAT_ANALYSER && net.n_classes == 2) {
-          const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
-          int64_t lblocks = (n_tiles + 3) / 4;
-          if (lblocks > ffn_num_cus()) lblocks = ffn_num_cus();
-          hipLaunchKernelGGL((ffn_lean_kernel<VAD_FEAT_ANALYSER>), dim3((int)lblocks), dim3(256), 0, st, net, in,
-                             n_rows, labels);
-          return hipGetLastError();
-        }
         if (VAD_FFN_GROUP >= 2 && mfcc_n == 13 && net.fragh && !net.logits && net.h1_bounded &&
             mode == VAD_FEAT_ANALYSER && net.n_classes == 2) {
           constexpr int NT = VAD_FFN_GROUP >= 2 ? VAD_FFN_GROUP : 2;
