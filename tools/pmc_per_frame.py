@@ -15,6 +15,7 @@ for label, key in (("mfcc_kernel (fp32, 26 mel, paired frames), per 1M-frame lau
                     "mfcc_kernel<float, 0, 13, true, 400, 1, 5, false>"),
                    ("mfcc_kernel (int16 PCM), per 1M-frame launch", "mfcc_kernel<short, 0, 13, true, 400, 1, 5, false>"),
                    ("ffn_wave_kernel (13-64-64-2 split-f16), per 1M-window launch", "ffn_wave_kernel<4, 4, 4, 1, 0, 2, 0, false>"),
+                   ("ffn_wave_group_kernel (13-64-64-2 tile pairs), per 1M-window launch", "ffn_wave_group_kernel<0, 2>"),
                    ("mfcc_ffn_kernel (fused, 13-64-64-2), per 1M-frame launch", "mfcc_ffn_kernel<float")):
     ks = [k for k in agg if key in k]
     if not ks:

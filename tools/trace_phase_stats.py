@@ -30,7 +30,7 @@ except (OSError, ValueError):
     pass
 out = {"last_n": last_n, "bench_kernels_ms": bench, "kernels": {}}
 for name, v in sorted(rows.items(), key=lambda kv: -sum(e - s for s, e, _ in kv[1])):
-    if len(v) < last_n + 1 or not ("mfcc_kernel" in name or "ffn_wave_kernel" in name or "mfcc_ffn_kernel" in name):
+    if len(v) < last_n + 1 or not ("mfcc_kernel" in name or "ffn_wave_kernel" in name or "ffn_wave_group_kernel" in name or "mfcc_ffn_kernel" in name):
         continue
     v.sort()
     tail, head = v[-last_n:], v[:-last_n]
