@@ -624,7 +624,8 @@ def test_fuzz_tree_windows(torch_cuda, depth, offline, F, seed):
     m = P.MfccPlan(O.get_mel_filterbanks(300, 8000, 512, 26, 16000)).clip_mfcc(torch.from_numpy(clip).cuda())
     mode = _lib.FEAT_OFFLINE if offline else _lib.FEAT_ANALYSER
     x = P.window_features(m, mode).cpu().numpy()
-    y = rng.integers(0, 2, len(x)) ^ (np.nan_to_num(x[:, 0]) > np.nanmedian(x[:, 0])).astype(int)
+    c0 = x[:, 0][~np.isnan(x[:, 0])]  # every window flat (all-NaN column): threshold 0
+    y = rng.integers(0, 2, len(x)) ^ (np.nan_to_num(x[:, 0]) > (np.median(c0) if len(c0) else 0.0)).astype(int)
     clf = DecisionTreeClassifier(max_depth=depth, random_state=0).fit(x, y)
     tree = TreeClassifier.from_sklearn(clf)
     got = tree.window_labels(m, mode).cpu().numpy()
