@@ -630,6 +630,31 @@ __global__ __launch_bounds__(64 * kGWpb) __attribute__((amdgpu_waves_per_eu(kGro
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4;
   const int jw = lane & 15;
+  const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
+  const int64_t total = (n_rows + 4) * MN;
+  const int64_t wave_id = (int64_t)blockIdx.x * kGWpb + wv;
+  const int64_t n_waves = (int64_t)gridDim.x * kGWpb;
+  auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
+    const int64_t base = t * (kWTile * MN);
+    const float* tb = mfcc + base;
+    const int64_t rem = total - 1 - base;
+    const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);
+#pragma unroll
+    for (int q = 0; q < kWRowRegs; ++q) {
+      const unsigned ob = 4u * (unsigned)(lane + 64 * q);
+      dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
+    }
+  };
+  // tile k of the group at t: t + k n_waves (clamped to t past the end:
+  // computed, not stored)
+  auto member = [&](int64_t t, int k) { return t + k * n_waves < n_tiles ? t + k * n_waves : t; };
+  // the first group's rows are requested before the block stages its tables,
+  // so the two latencies overlap
+  float pre[NT][kWRowRegs];
+  if (wave_id < n_tiles) {
+#pragma unroll
+    for (int k = 0; k < NT; ++k) load(member(wave_id, k), pre[k]);
+  }
   // the slot table (biases, output-layer weights, the class-1 minus class-0
   // difference) and the split-f16 fragments, as in ffn_wave_kernel's kAll
   {
@@ -661,30 +686,7 @@ __global__ __launch_bounds__(64 * kGWpb) __attribute__((amdgpu_waves_per_eu(kGro
   for (int k = 0; k < NT; ++k)
     for (int i = lane; i < kWTile * XS; i += 64) x_s[wv][k][i] = 0.f;  // columns 13.. stay 0
 
-  const int64_t n_tiles = (n_rows + kWTile - 1) / kWTile;
-  const int64_t total = (n_rows + 4) * MN;
-  const int64_t wave_id = (int64_t)blockIdx.x * kGWpb + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * kGWpb;
-  auto load = [&](int64_t t, float (&dst)[kWRowRegs]) {
-    const int64_t base = t * (kWTile * MN);
-    const float* tb = mfcc + base;
-    const int64_t rem = total - 1 - base;
-    const unsigned limb = 4u * (unsigned)(rem < kWRows ? rem : kWRows);
-#pragma unroll
-    for (int q = 0; q < kWRowRegs; ++q) {
-      const unsigned ob = 4u * (unsigned)(lane + 64 * q);
-      dst[q] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(tb) + (ob < limb ? ob : limb));
-    }
-  };
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0
-  // tile k of the group at t: t + k n_waves (clamped to t past the end:
-  // computed, not stored)
-  auto member = [&](int64_t t, int k) { return t + k * n_waves < n_tiles ? t + k * n_waves : t; };
-  float pre[NT][kWRowRegs];
-  if (wave_id < n_tiles) {
-#pragma unroll
-    for (int k = 0; k < NT; ++k) load(member(wave_id, k), pre[k]);
-  }
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt 0: no staging-load waits left for the loop body
   for (int64_t t = wave_id; t < n_tiles; t += NT * n_waves) {
     const int64_t tn = t + NT * n_waves < n_tiles ? t + NT * n_waves : t;
     wave_lds_handoff();
