@@ -287,16 +287,36 @@ int vad_mfcc_plan_create(const double* fb, int32_t n_filters, int32_t fft_n, int
     if (e == hipSuccess) e = hipMemcpy(p->tw_gen, tw.data(), tw.size() * sizeof(double2), hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(p->tw_gen); free(p); return (int)e; }
   }
-  // the streaming hop kernel's tables as one block: W512^k (256 complex),
-  // f_lo / f_len / f_off (as int bits), the taps, the DCT rows at stride nf
-  p->n_taps = off;
+  // the streaming hop kernel's tables as one block: W512^k (256 complex);
+  // per filter its first bin rounded down to 4, its tap count from there
+  // rounded up to 4 and its row offset (as int bits); the 16-B aligned tap
+  // rows (the filter's taps at their bins, zero around them: a lane reads
+  // four taps and four power bins per pair of 16-B reads, and the zero taps
+  // add +0 to a sum of non-negative terms); the DCT rows
+  std::vector<float> rows;
+  std::vector<int> lo4(n_filters), n4(n_filters), off4(n_filters);
+  for (int m = 0; m < n_filters; ++m) {
+    const int lo = h.f_lo[m], n = h.f_len[m];
+    lo4[m] = lo & ~3;
+    n4[m] = n > 0 ? ((lo + n + 3) & ~3) - lo4[m] : 0;
+    off4[m] = (int)rows.size();
+    for (int t = 0; t < n4[m]; ++t) {
+      const int bin = lo4[m] + t;
+      rows.push_back(bin >= lo && bin < lo + n ? h.taps[h.f_off[m] + bin - lo] : 0.f);
+    }
+  }
+  p->n_taps = (int)rows.size();  // a multiple of 4
   std::vector<float> blob;
   for (int k = 0; k < 256; ++k) { blob.push_back(h.tw_b[k].x); blob.push_back(h.tw_b[k].y); }
-  for (const int* arr : {h.f_lo, h.f_len, h.f_off})
-    for (int m = 0; m < n_filters; ++m) { float f; memcpy(&f, &arr[m], 4); blob.push_back(f); }
-  blob.insert(blob.end(), h.taps, h.taps + off);
+  for (const std::vector<int>* arr : {&lo4, &n4, &off4})
+    for (int m = 0; m < n_filters; ++m) { float f; memcpy(&f, &(*arr)[m], 4); blob.push_back(f); }
+  while (blob.size() % 4) blob.push_back(0.f);
+  blob.insert(blob.end(), rows.begin(), rows.end());
+  // the DCT rows (16-B aligned: every tap row is a multiple of 4 floats) at
+  // stride vec_row_stride(nf), zero padded
   for (int c = 0; c < mfcc_n; ++c)
-    for (int m = 0; m < n_filters; ++m) blob.push_back(h.dct[c * kMaxFilters + m]);
+    for (int m = 0; m < vec_row_stride(n_filters); ++m)
+      blob.push_back(m < n_filters ? h.dct[c * kMaxFilters + m] : 0.f);
   while (blob.size() % 4) blob.push_back(0.f);
   p->hop_blob_n = (int)blob.size();
   hipError_t e = hipMalloc((void**)&p->hop_blob, blob.size() * sizeof(float));
@@ -526,18 +546,34 @@ int vad_ffn_plan_create(int32_t n_layers, const int32_t* dims, const float* cons
     }
   }
 
-  // the weights as given: W_l (in, out) row-major, then b_l
+  // the streaming forward's weights (FfnDev::wraw): first the weights as
+  // given, W_l (in, out) row-major then b_l, with zero rows past the last
+  // layer; then each W_l transposed from that flat array, row o holding
+  // flat[W_l + k dout + o] for k < din rounded up to 4 -- past din these are
+  // the same values (the next rows of the flat array) a four-at-a-time read
+  // of the (in, out) layout met, against zero inputs, so the forward's
+  // arithmetic is unchanged -- and the biases
+  std::vector<float> flat;
+  int flat_w[VAD_MAX_FFN_LAYERS], flat_b[VAD_MAX_FFN_LAYERS];
+  for (int l = 0; l < n_layers; ++l) {
+    flat_w[l] = (int)flat.size();
+    flat.insert(flat.end(), W[l], W[l] + (size_t)dims[l] * dims[l + 1]);
+    flat_b[l] = (int)flat.size();
+    flat.insert(flat.end(), b[l], b[l] + dims[l + 1]);
+  }
+  flat.insert(flat.end(), 3 * 64 + 4, 0.f);
   std::vector<float> wraw;
   for (int l = 0; l < n_layers; ++l) {
+    const int din = dims[l], dout = dims[l + 1], S = vec_row_stride(din);
+    net.wstride[l] = S;
     net.woff[l] = (int)wraw.size();
-    wraw.insert(wraw.end(), W[l], W[l] + (size_t)dims[l] * dims[l + 1]);
+    for (int o = 0; o < dout; ++o)
+      for (int k = 0; k < S; ++k)
+        wraw.push_back(k < ((din + 3) & ~3) ? flat[flat_w[l] + (size_t)k * dout + o] : 0.f);
     net.boff[l] = (int)wraw.size();
-    wraw.insert(wraw.end(), b[l], b[l] + dims[l + 1]);
+    wraw.insert(wraw.end(), b[l], b[l] + dout);
+    while (wraw.size() % 4) wraw.push_back(0.f);
   }
-  // zero rows past the last layer (the streaming forward reads its inputs in
-  // fours: up to three weight rows past W_l), whole 16-B vectors
-  wraw.insert(wraw.end(), 3 * 64 + 4, 0.f);
-  while (wraw.size() % 4) wraw.push_back(0.f);
   net.wraw_n = (int)wraw.size();
   // layer-1 inputs of a 13-input network on analyser features (|Mn| <=
   // sqrt(5), ffn_dev.h wave_tile_in_bounded): bounded by max_j |b0_j| +

@@ -161,8 +161,8 @@ struct HopTables {
   const int* f_len;
   const int* f_off;
   const float* taps;
-  const float* dct;  // [c][m], stride nf
-  const float* w;    // the FFN weights as given (FfnDev::wraw layout)
+  const float* dct;  // [c][m], stride vec_row_stride(nf), 16-B aligned
+  const float* w;    // the FFN weights (FfnDev::wraw: transposed rows)
 };
 
 __device__ __forceinline__ float2 cmulf(float2 a, float2 w) {
@@ -178,6 +178,9 @@ __device__ __forceinline__ float2 w256(const float2* __restrict__ tw, int m) {
 // NR: 64-sample chunks of the frame a lane holds (7: frames up to 448
 // samples, the reference's 400; 16: up to 1024) -- the frame and the next
 // hop's samples stay in registers across hops, so the bound matters
+#ifndef VAD_HOP_DIAG_SKIP
+#define VAD_HOP_DIAG_SKIP 0  // timing only (wrong labels): 1 skips the FFN, 2 also the mel / DCT
+#endif
 template <int NR>
 __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restrict__ blob, int blob_n, int nf,
                                                           int n_taps, FfnDev net,
@@ -217,7 +220,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
   T.f_lo = ilo;
   T.f_len = ilo + nf;
   T.f_off = ilo + 2 * nf;
-  T.taps = base + 2 * 256 + 3 * nf;
+  T.taps = base + ((2 * 256 + 3 * nf + 3) & ~3);  // 16-B aligned rows of n_taps (a multiple of 4) in all
   T.dct = T.taps + n_taps;
   T.w = base + blob_n;
 
@@ -364,22 +367,42 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     for (int q = 0; q < 4; ++q) pw[ln + 64 * q] = pk[q];
     asm volatile("" ::: "memory");
     // -- mel + log10 (ln m), lifter x DCT (ln c)
-    if (ln < nf) {
-      const int lo = T.f_lo[ln], n = T.f_len[ln];
-      const float* wt = T.taps + T.f_off[ln];
-      // unrolled: the LDS reads of a batch are in flight together (a rolled
-      // loop waits one LDS round trip per tap)
+    if (VAD_HOP_DIAG_SKIP < 2 && ln < nf) {
+      // the filter's 16-B aligned tap row against the power bins from its
+      // first bin rounded down to 4: four taps per pair of 16-B reads, one
+      // fma chain in bin order (the zero taps around the filter add +0)
+      const int lo4 = T.f_lo[ln], n4 = T.f_len[ln];
+      const float4* wt4 = reinterpret_cast<const float4*>(T.taps + T.f_off[ln]);
+      const float4* pw4 = reinterpret_cast<const float4*>(pw + lo4);
       float e = 0.f;
-#pragma unroll 8
-      for (int t = 0; t < n; ++t) e = fmaf(wt[t], pw[lo + t], e);
+#pragma unroll 2
+      for (int t = 0; t < n4; t += 4) {
+        const float4 w = wt4[t >> 2], q = pw4[t >> 2];
+        e = fmaf(w.x, q.x, e);
+        e = fmaf(w.y, q.y, e);
+        e = fmaf(w.z, q.z, e);
+        e = fmaf(w.w, q.w, e);
+      }
       lmr[ln] = log10_pos(e == 0.f ? 0x1p-52f : e);  // mfcc.py:74-75
     }
     asm volatile("" ::: "memory");
     float mf = 0.f;
-    if (ln < mfcc_n) {
-      const float* d = T.dct + ln * nf;
-#pragma unroll 8
-      for (int m = 0; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
+    if (VAD_HOP_DIAG_SKIP < 2 && ln < mfcc_n) {
+      // one fma chain in m order; four terms per pair of 16-B reads (the
+      // lane's row, the log-mel row broadcast)
+      const float4* d4 = reinterpret_cast<const float4*>(T.dct + ln * vec_row_stride(nf));
+      const float4* l4 = reinterpret_cast<const float4*>(lmr);
+      int m = 0;
+#pragma unroll 4
+      for (; m + 4 <= nf; m += 4) {
+        const float4 d = d4[m >> 2], l = l4[m >> 2];
+        mf = fmaf(d.x, l.x, mf);
+        mf = fmaf(d.y, l.y, mf);
+        mf = fmaf(d.z, l.z, mf);
+        mf = fmaf(d.w, l.w, mf);
+      }
+      const float* d = T.dct + ln * vec_row_stride(nf);
+      for (; m < nf; ++m) mf = fmaf(d[m], lmr[m], mf);
     }
     // -- window of the five previous frames, then push the new row
     const bool have = c >= 5;
@@ -414,7 +437,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     }
     asm volatile("" ::: "memory");
     uint8_t label = 255;
-    if (have) {
+    if (VAD_HOP_DIAG_SKIP == 0 && have) {
       // -- FFN: exact f32, ln o of each layer
       float* hin = act_a;
       float* hout = act_b;
@@ -424,17 +447,18 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
         // four inputs per step (one ds_read_b128 broadcast), four partial
         // sums; inputs past din are zero and the weight rows past W_l read
         // the next finite values of the block (zero-padded at its end)
-        const float* W = T.w + net.woff[l];
+        // the lane's transposed row: four weights per 16-B read
+        const float4* w4 = reinterpret_cast<const float4*>(T.w + net.woff[l] + ln * net.wstride[l]);
         float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
         if (ln < dout) {
           const float4* h4 = reinterpret_cast<const float4*>(hin);
 #pragma unroll 4
           for (int kq = 0; kq < din; kq += 4) {
-            const float4 h = h4[kq >> 2];
-            a0 = fmaf(W[kq * dout + ln], h.x, a0);
-            a1 = fmaf(W[(kq + 1) * dout + ln], h.y, a1);
-            a2 = fmaf(W[(kq + 2) * dout + ln], h.z, a2);
-            a3 = fmaf(W[(kq + 3) * dout + ln], h.w, a3);
+            const float4 h = h4[kq >> 2], w = w4[kq >> 2];
+            a0 = fmaf(w.x, h.x, a0);
+            a1 = fmaf(w.y, h.y, a1);
+            a2 = fmaf(w.z, h.z, a2);
+            a3 = fmaf(w.w, h.w, a3);
           }
         }
         const float acc = T.w[net.boff[l] + (ln < dout ? ln : 0)] + ((a0 + a1) + (a2 + a3));

@@ -62,12 +62,17 @@ struct FfnDev {
   // optional (tests): the fp32 logits of every classified row,
   // logits[row * n_classes + c] (null: labels only)
   float* logits;
-  // the Keras weights as given (W_l (in, out) row-major, then b_l), for the
-  // one-wave-per-stream VALU forward of the streaming hop kernel
+  // the Keras weights for the one-wave-per-stream VALU forward of the
+  // streaming hop kernel: per layer W_l transposed, row o (output unit o)
+  // at woff + o * wstride holding W_l[k][o] for k < din rounded up to 4
+  // (wstride = that, or 4 more, so that wstride / 4 is odd: lanes reading
+  // their rows as 16-B vectors hit every LDS bank once per 16 lanes), then
+  // b_l at boff
   const float* wraw;
   int wraw_n;  // floats in wraw
   int woff[VAD_MAX_FFN_LAYERS];
   int boff[VAD_MAX_FFN_LAYERS];
+  int wstride[VAD_MAX_FFN_LAYERS];
   // 1: with analyser inputs (|Mn| <= sqrt(5), or a NaN / inf the kernels
   // handle as they come) every finite layer-1 input is below 32768 in
   // magnitude, so that layer needs no f16-range check (capi.hip, from the
@@ -193,5 +198,12 @@ __device__ __forceinline__ float log10_pos(float e) {
 
 // NaN-keeping ReLU (numpy / Keras keep NaN; fmaxf would drop it).
 __device__ __forceinline__ float relu_nan(float x) { return x < 0.f ? 0.f : x; }
+
+// Floats per row of a table whose rows lanes read as 16-B vectors: n rounded
+// up to 4, plus 4 when that is a multiple of 8 (a stride of 4 x odd floats
+// puts 16 consecutive lanes' vectors on distinct LDS banks)
+__host__ __device__ constexpr int vec_row_stride(int n) {
+  return ((n + 3) & ~3) % 8 == 0 ? ((n + 3) & ~3) + 4 : ((n + 3) & ~3);
+}
 
 }  // namespace vad
