@@ -178,9 +178,6 @@ __device__ __forceinline__ float2 w256(const float2* __restrict__ tw, int m) {
 // NR: 64-sample chunks of the frame a lane holds (7: frames up to 448
 // samples, the reference's 400; 16: up to 1024) -- the frame and the next
 // hop's samples stay in registers across hops, so the bound matters
-#ifndef VAD_HOP_DIAG_SKIP
-#define VAD_HOP_DIAG_SKIP 0  // timing only (wrong labels): 1 skips the FFN, 2 also the mel / DCT
-#endif
 template <int NR>
 __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restrict__ blob, int blob_n, int nf,
                                                           int n_taps, FfnDev net,
@@ -367,7 +364,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     for (int q = 0; q < 4; ++q) pw[ln + 64 * q] = pk[q];
     asm volatile("" ::: "memory");
     // -- mel + log10 (ln m), lifter x DCT (ln c)
-    if (VAD_HOP_DIAG_SKIP < 2 && ln < nf) {
+    if (ln < nf) {
       // the filter's 16-B aligned tap row against the power bins from its
       // first bin rounded down to 4: four taps per pair of 16-B reads, one
       // fma chain in bin order (the zero taps around the filter add +0)
@@ -387,7 +384,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     }
     asm volatile("" ::: "memory");
     float mf = 0.f;
-    if (VAD_HOP_DIAG_SKIP < 2 && ln < mfcc_n) {
+    if (ln < mfcc_n) {
       // one fma chain in m order; four terms per pair of 16-B reads (the
       // lane's row, the log-mel row broadcast)
       const float4* d4 = reinterpret_cast<const float4*>(T.dct + ln * vec_row_stride(nf));
@@ -437,7 +434,7 @@ __global__ __launch_bounds__(1024) void stream_hop_kernel(const float* __restric
     }
     asm volatile("" ::: "memory");
     uint8_t label = 255;
-    if (VAD_HOP_DIAG_SKIP == 0 && have) {
+    if (have) {
       // -- FFN: exact f32, ln o of each layer
       float* hin = act_a;
       float* hout = act_b;
